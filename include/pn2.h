@@ -1,0 +1,148 @@
+/*
+ * pn2.h -- C ABI of libpn2.so, the MI355X (gfx950) PointNet++ set-abstraction path.
+ *
+ * Every entry point:
+ *   - takes plain pointers to caller-allocated DEVICE buffers (the caller's allocator owns all
+ *     memory; nothing here allocates), element strides as int64, and a hipStream_t passed as
+ *     void*;
+ *   - is asynchronous on that stream and never synchronises the device, so it may be captured
+ *     into a hipGraph;
+ *   - returns PN2_OK (0) or a negative PN2_E* code; the message of the last failure on the
+ *     calling thread is returned by pn2_last_error() (thread-local: the library holds no other
+ *     mutable global state, so it is re-entrant across host threads, as the reference's
+ *     concurrent-inference demo /root/reference/mutilthreading/predict_test.py:44-63 requires).
+ *
+ * Reference interfaces replaced (file:line in /root/reference):
+ *   pn2_fps_f32            farthest_point_sample            model/pointnet2_utils.py:47-68
+ *                          (+ index_points(points, fps_idx)  model/pointnet2_utils.py:106)
+ *   pn2_ball_query_f32     query_ball_point + square_distance model/pointnet2_utils.py:70-90, 5-26
+ *   pn2_pack_points_f32    torch.sum(points**2,-1) of square_distance model/pointnet2_utils.py:24-25
+ *   pn2_square_distance_f32 square_distance                  model/pointnet2_utils.py:5-26
+ *   pn2_index_points_f32   index_points                      model/pointnet2_utils.py:28-45
+ *   pn2_group_f32          grouping of sample_and_group /    model/pointnet2_utils.py:107-116,
+ *                          PointNetSetAbstractionMsg         model/pointnet2_utils.py:204-209
+ *   pn2_pack_layer_f32     Conv2d(1x1)+BatchNorm2d(eval) params of the shared MLP
+ *                                                            model/pointnet2_utils.py:150-156, 184-193
+ *   pn2_sa_mlp_max_f32     grouped shared MLP (conv+bn+relu)* + max over the neighbourhood
+ *                                                            model/pointnet2_utils.py:167-172, 211-218
+ */
+#ifndef PN2_H
+#define PN2_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PN2_OK 0
+#define PN2_EINVAL (-1)     /* bad argument / shape */
+#define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
+#define PN2_EHIP (-3)       /* HIP runtime error at launch */
+
+#define PN2_ABI_VERSION 1
+
+int pn2_abi_version(void);
+const char *pn2_last_error(void);
+
+/* Packed point layout used by the ball query: [B][N][cp] float32, cp = pn2_packed_stride(C),
+ * holding the C coordinates, then ssq = torch.sum(p**2,-1) computed with the reference's
+ * layout-dependent CPU summation order, then zero padding. */
+int64_t pn2_packed_stride(int64_t C);
+
+/* Farthest point sampling over points[b, n, c] = pts[b*sb + n*sn + c*sc].
+ * start[B] (int64, device) = the reference's torch.randint draw.  Outputs (device):
+ *   out_idx    [B,S] int64                      fps indices
+ *   out_pts    [B,S,C] float32 contiguous, or NULL   index_points(points, fps_idx)
+ *   out_packed [B,S,cp] float32, or NULL         packed centroids (contiguous-layout ssq)
+ *   pts_packed [B,N,cp] float32, or NULL         packed input points (input-layout ssq)
+ * Requires N <= 32768 and C <= 16. */
+int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+                int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
+                float *out_packed, float *pts_packed, void *stream);
+
+/* Pack a [B,N,C] strided view into [B,N,cp] with its ssq (see above). */
+int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,
+                        int64_t sn, int64_t sc, float *packed, void *stream);
+
+/* query_ball_point: for every centroid, the first K point indices (ascending) whose
+ * square_distance is not > (float)(radius*radius), padded with the first hit (N if none).
+ * pts_packed [B,N,cp], ctr_packed [B,S,cp] from pn2_pack_points_f32 / pn2_fps_f32.
+ * out_idx [B,S,K] int64.  K > N is rejected with PN2_EINVAL (the reference raises IndexError). */
+int pn2_ball_query_f32(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N,
+                       int64_t S, int64_t C, double radius, int64_t K, int64_t *out_idx,
+                       void *stream);
+
+/* square_distance(src, dst) -> out [B,S,N] float32 from packed records of src [B,S,cp] and
+ * dst [B,N,cp] (same float32 recipe as the ball query). */
+int pn2_square_distance_f32(const float *src_packed, const float *dst_packed, int64_t B,
+                            int64_t S, int64_t N, int64_t C, float *out, void *stream);
+
+/* out[b, m, :] = pts[b, idx[b*M + m], :] ; out contiguous [B,M,C]. idx int64 [B,M]. */
+int pn2_index_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,
+                         int64_t sn, int64_t sc, const int64_t *idx, int64_t M, float *out,
+                         void *stream);
+
+/* Grouping: out[b,s,k,:] (contiguous [B,S,K,C+D]) =
+ *   feature_first == 0 : [pts[b,idx]-ctr[b,s], feat[b,idx]]   (sample_and_group, SSG)
+ *   feature_first == 1 : [feat[b,idx], pts[b,idx]-ctr[b,s]]   (PointNetSetAbstractionMsg)
+ * feat may be NULL (D = 0).  ctr is contiguous [B,S,C]; feat element (b,n,d) at
+ * feat[b*fb + n*fn + d*fd]. */
+int pn2_group_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+                  int64_t sc, const float *feat, int64_t D, int64_t fb, int64_t fn, int64_t fd,
+                  const float *ctr, int64_t S, const int64_t *idx, int64_t K, int feature_first,
+                  float *out, void *stream);
+
+/* One shared-MLP layer packed for the kernel: wt [cin_pad][cout] (= W^T, zero rows past cin),
+ * alpha[cout], beta[cout] such that layer(x) = relu(alpha * (W x) + beta), i.e. the eval-mode
+ * BatchNorm2d folded with the conv bias.  cin_pad = pn2_layer_cin_pad(cin). */
+int64_t pn2_layer_cin_pad(int64_t cin);
+int pn2_pack_layer_f32(const float *W, const float *bias, const float *gamma, const float *beta,
+                       const float *mean, const float *var, double eps, int64_t cout,
+                       int64_t cin, float *wt, float *alpha, float *beta_out, void *stream);
+
+/* Source of the MLP's input rows. */
+#define PN2_SRC_GROUP_XYZ_FIRST 0  /* sample_and_group:  [xyz-ctr, feat] rows of group idx   */
+#define PN2_SRC_GROUP_FEAT_FIRST 1 /* MSG:               [feat, xyz-ctr] rows of group idx   */
+#define PN2_SRC_GROUP_ALL 2        /* sample_and_group_all: [xyz (raw), feat] of every point */
+#define PN2_SRC_ROWS 3             /* a dense [M][cin] float32 matrix (row stride rs)        */
+
+typedef struct pn2_mlp_layer {
+    const float *wt;    /* [cin_pad][cout] */
+    const float *alpha; /* [cout] */
+    const float *beta;  /* [cout] */
+    int64_t cin;
+    int64_t cout;
+} pn2_mlp_layer;
+
+typedef struct pn2_sa_src {
+    int mode; /* PN2_SRC_* */
+    const float *pts; int64_t pb, pn, pc; /* points [B,N,C], any strides            */
+    const float *feat; int64_t fb, fn;    /* features [B,N,D], channel stride 1, or NULL */
+    const float *ctr;                     /* centroids [B,S,C] contiguous (group modes) */
+    const int64_t *idx;                   /* [B,S,K] int64 contiguous (group modes)     */
+    const float *rows; int64_t rs;        /* PN2_SRC_ROWS: [M][rs]                      */
+    int64_t B, N, C, D, S, K;             /* rows M = B*S*K (GROUP_ALL: S=1, K=N)       */
+} pn2_sa_src;
+
+/* Bytes of workspace pn2_sa_mlp_max_f32 needs for this layer chain: 0 when the chain runs as
+ * one fused kernel (every hidden width <= 256 and a compiled tile signature), otherwise two
+ * [M][max hidden width] float32 buffers for the layer-by-layer path.  -1 on invalid input. */
+int64_t pn2_sa_mlp_workspace_bytes(const pn2_sa_src *src, const pn2_mlp_layer *layers,
+                                   int nlayers);
+
+/* Fused gather -> nlayers x (1x1 conv + BN + ReLU) -> output.
+ *   pool != 0 : out[g*ostride + c] = max over the K rows of group g (g = b*S+s) -- the
+ *               torch.max(new_feature, 2)[0] of the reference, stored channels-last.
+ *   pool == 0 : out[row*ostride + c] (dense rows, feeds a following PN2_SRC_ROWS call).
+ * nlayers in [1,4]; every cout must be a multiple of 32.  Hidden activations stay in LDS; the
+ * last layer is computed in 256-column slices (and split over the grid when nlayers == 1).
+ * workspace may be NULL when pn2_sa_mlp_workspace_bytes() returns 0. */
+int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers, int nlayers,
+                       int pool, float *out, int64_t ostride, float *workspace,
+                       int64_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PN2_H */

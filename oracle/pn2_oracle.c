@@ -1,0 +1,181 @@
+/*
+ * pn2_oracle.c -- CPU restatement of the PointNet++ set-abstraction index path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker.  The product
+ * (libpn2.so + the pn2 package) never links, loads or calls it.
+ *
+ * It restates, with the exact float32 rounding sequence of the reference's
+ * PyTorch-CPU execution (torch 2.10 CPU, capability AVX512, MKL sgemm):
+ *   farthest_point_sample   /root/reference/model/pointnet2_utils.py:47-68
+ *   square_distance         /root/reference/model/pointnet2_utils.py:5-26
+ *   query_ball_point        /root/reference/model/pointnet2_utils.py:70-90
+ *
+ * Rounding rules (pinned against the imported reference, see
+ * tests/golden/make_goldens.py and tests/test_oracle_golden.py):
+ *   - torch.sum(x**2, -1) over the channel axis depends on the memory layout of x:
+ *       channel-contiguous rows ("contig", stride_c == 1):
+ *         C < 8  : ATen row_sum with 4 accumulators, tail into acc0, then acc0+acc1+acc2+acc3
+ *         C >= 8 : 8 lane partials over C/8 chunks, scalar tail summed first, then
+ *                  tail + v0 + v1 + ... + v7 (sequential)
+ *       point-contiguous rows ("strided", stride_n == 1, i.e. the permute(0,2,1) view of a
+ *       [B,C,N] tensor): points n < 16*floor(N/16) are summed sequentially over c, the
+ *       scalar tail n >= 16*floor(N/16) uses the row_sum order above.
+ *   - matmul(src, dst^T) = fmaf chain in k order starting from s0*d0 (MKL sgemm), except when
+ *     S*N*C < 400, where ATen's naive bmm kernel accumulates unfused: ((0 + s0*d0) + s1*d1) ...
+ *   - square_distance = ((-2*mm) + ssq(src)) + ssq(dst), each rounded to float32.
+ *   - FPS: dist init 1e10f, update on strict '<', argmax returns the first maximum.
+ *   - ball query: compare in float32 against (float)(r*r); first K hits in index order;
+ *     pad with the first hit (or N when there is none).
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+static float rowsum4(const float *a, int64_t C) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int64_t n = C / 4, i, k;
+    for (i = 0; i < n; ++i)
+        for (k = 0; k < 4; ++k) acc[k] = acc[k] + a[4 * i + k];
+    for (i = 4 * n; i < C; ++i) acc[0] = acc[0] + a[i];
+    return ((acc[0] + acc[1]) + acc[2]) + acc[3];
+}
+
+static float seqsum(const float *a, int64_t C) {
+    float r = 0.f;
+    for (int64_t i = 0; i < C; ++i) r = r + a[i];
+    return r;
+}
+
+static float contigsum(const float *a, int64_t C) {
+    if (C < 8) return rowsum4(a, C);
+    int64_t nv = C / 8, i, k;
+    float v[8];
+    for (k = 0; k < 8; ++k) {
+        float s = 0.f;
+        for (i = 0; i < nv; ++i) s = s + a[8 * i + k];
+        v[k] = s;
+    }
+    float r = seqsum(a + 8 * nv, C - 8 * nv);
+    for (k = 0; k < 8; ++k) r = r + v[k];
+    return r;
+}
+
+/* Sum of the C squared channel values of point n under the reference's layout rule. */
+static float layout_sum(const float *sq, int64_t C, int64_t n, int64_t N, int strided) {
+    if (strided) return (n < (N / 16) * 16) ? seqsum(sq, C) : rowsum4(sq, C);
+    return contigsum(sq, C);
+}
+
+static int is_strided(int64_t sn, int64_t sc) { return sc != 1 && sn == 1; }
+
+#define MAXC 4096
+
+/* ssq[b,n] = torch.sum(points**2, -1) for a [B,N,C] view with the given element strides. */
+void pn2o_ssq(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+              int64_t sc, float *out) {
+    float sq[MAXC];
+    int strided = is_strided(sn, sc);
+    for (int64_t b = 0; b < B; ++b)
+        for (int64_t n = 0; n < N; ++n) {
+            const float *p = pts + b * sb + n * sn;
+            for (int64_t c = 0; c < C; ++c) sq[c] = p[c * sc] * p[c * sc];
+            out[b * N + n] = layout_sum(sq, C, n, N, strided);
+        }
+}
+
+/* farthest_point_sample (pointnet2_utils.py:47-68).  out[b,i] int64. */
+void pn2o_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+              int64_t sc, const int64_t *start, int64_t S, int64_t *out) {
+    float *dist = (float *)malloc(sizeof(float) * (size_t)N);
+    float sq[MAXC];
+    int strided = is_strided(sn, sc);
+    for (int64_t b = 0; b < B; ++b) {
+        const float *P = pts + b * sb;
+        for (int64_t n = 0; n < N; ++n) dist[n] = 1e10f;
+        int64_t far = start[b];
+        for (int64_t i = 0; i < S; ++i) {
+            out[b * S + i] = far;
+            const float *c = P + far * sn;
+            for (int64_t n = 0; n < N; ++n) {
+                const float *p = P + n * sn;
+                for (int64_t k = 0; k < C; ++k) {
+                    float d = p[k * sc] - c[k * sc];
+                    sq[k] = d * d;
+                }
+                float d = layout_sum(sq, C, n, N, strided);
+                if (d < dist[n]) dist[n] = d;
+            }
+            int64_t best = 0;
+            float bv = dist[0];
+            for (int64_t n = 1; n < N; ++n)
+                if (dist[n] > bv) { bv = dist[n]; best = n; }
+            far = best;
+        }
+    }
+    free(dist);
+}
+
+/* square_distance(src, dst) (pointnet2_utils.py:5-26) for one (b, s, n) triple. */
+static float sqdist(const float *s, int64_t ssc, const float *d, int64_t dsc, int64_t C,
+                    float ssq_s, float ssq_d, int small) {
+    float mm = s[0] * d[0];
+    if (small) {
+        for (int64_t k = 1; k < C; ++k) mm = mm + s[k * ssc] * d[k * dsc];
+    } else {
+        for (int64_t k = 1; k < C; ++k) mm = fmaf(s[k * ssc], d[k * dsc], mm);
+    }
+    float t = (-2.0f * mm) + ssq_s;
+    return t + ssq_d;
+}
+
+/* query_ball_point (pointnet2_utils.py:70-90).  Returns 0, or -1 if K > N
+ * (the reference raises IndexError there). */
+int pn2o_ball_query(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+                    int64_t sc, const float *ctr, int64_t S, int64_t cb, int64_t cs, int64_t cc,
+                    double radius, int64_t K, int64_t *out) {
+    if (K > N) return -1;
+    float r2 = (float)(radius * radius);
+    int small = S * N * C < 400;
+    float *ssq_p = (float *)malloc(sizeof(float) * (size_t)(B * N));
+    float *ssq_c = (float *)malloc(sizeof(float) * (size_t)(B * S));
+    pn2o_ssq(pts, B, N, C, sb, sn, sc, ssq_p);
+    pn2o_ssq(ctr, B, S, C, cb, cs, cc, ssq_c);
+    for (int64_t b = 0; b < B; ++b)
+        for (int64_t s = 0; s < S; ++s) {
+            int64_t *o = out + (b * S + s) * K;
+            int64_t cnt = 0;
+            const float *q = ctr + b * cb + s * cs;
+            for (int64_t n = 0; n < N && cnt < K; ++n) {
+                float d = sqdist(q, cc, pts + b * sb + n * sn, sc, C, ssq_c[b * S + s],
+                                 ssq_p[b * N + n], small);
+                if (!(d > r2)) o[cnt++] = n;
+            }
+            int64_t first = cnt ? o[0] : N;
+            for (int64_t k = cnt; k < K; ++k) o[k] = first;
+        }
+    free(ssq_p);
+    free(ssq_c);
+    return 0;
+}
+
+/* Full square_distance matrix [B,S,N] (used by the tests to pin the recipe). */
+void pn2o_square_distance(const float *src, int64_t B, int64_t S, int64_t C, int64_t ab,
+                          int64_t as, int64_t ac, const float *dst, int64_t N, int64_t db,
+                          int64_t dn, int64_t dc, float *out) {
+    float *ssq_s = (float *)malloc(sizeof(float) * (size_t)(B * S));
+    float *ssq_d = (float *)malloc(sizeof(float) * (size_t)(B * N));
+    pn2o_ssq(src, B, S, C, ab, as, ac, ssq_s);
+    pn2o_ssq(dst, B, N, C, db, dn, dc, ssq_d);
+    int small = S * N * C < 400;
+    for (int64_t b = 0; b < B; ++b)
+        for (int64_t s = 0; s < S; ++s)
+            for (int64_t n = 0; n < N; ++n)
+                out[(b * S + s) * N + n] = sqdist(src + b * ab + s * as, ac, dst + b * db + n * dn,
+                                                  dc, C, ssq_s[b * S + s], ssq_d[b * N + n], small);
+    free(ssq_s);
+    free(ssq_d);
+}

@@ -1,0 +1,88 @@
+// group.hip -- index_points and the neighbourhood grouping, for the public op API.
+//
+// index_points:        /root/reference/model/pointnet2_utils.py:28-45
+// sample_and_group:    pointnet2_utils.py:107-116  ([xyz - centroid, feature], xyz first)
+// SA-MSG grouping:     pointnet2_utils.py:204-209  ([feature, xyz - centroid], feature first)
+// The fused SA path (sa_mlp.hip) gathers straight into LDS and never materialises these
+// tensors; these kernels serve the standalone functions of the drop-in module.
+// One thread per output element (contiguous output => coalesced stores); the subtraction is a
+// single correctly rounded float32 op, bit-identical to the reference.
+#include "pn2_internal.h"
+
+namespace pn2 {
+
+__global__ __launch_bounds__(256) void index_points_kernel(const float *__restrict__ pts,
+                                                           int64_t B, int64_t N, int64_t C,
+                                                           int64_t sb, int64_t sn, int64_t sc,
+                                                           const int64_t *__restrict__ idx,
+                                                           int64_t M, float *__restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= B * M * C) return;
+    const int64_t c = e % C;
+    const int64_t bm = e / C;
+    const int64_t b = bm / M;
+    const int64_t n = idx[bm];
+    out[e] = pts[b * sb + n * sn + c * sc];
+}
+
+__global__ __launch_bounds__(256) void group_kernel(const float *__restrict__ pts, int64_t N,
+                                                    int64_t C, int64_t sb, int64_t sn, int64_t sc,
+                                                    const float *__restrict__ feat, int64_t D,
+                                                    int64_t fb, int64_t fn, int64_t fd,
+                                                    const float *__restrict__ ctr, int64_t S,
+                                                    const int64_t *__restrict__ idx, int64_t K,
+                                                    int feature_first, int64_t total,
+                                                    float *__restrict__ out) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int64_t W = C + D;
+    const int64_t ch = e % W;
+    const int64_t row = e / W;  // (b*S + s)*K + k
+    const int64_t g = row / K;
+    const int64_t b = g / S;
+    const int64_t n = idx[row];
+    const int64_t xc = feature_first ? ch - D : ch;  // xyz channel, if any
+    float v;
+    if (xc >= 0 && xc < C)
+        v = __fsub_rn(pts[b * sb + n * sn + xc * sc], ctr[g * C + xc]);
+    else {
+        const int64_t d = feature_first ? ch : ch - C;
+        v = feat[b * fb + n * fn + d * fd];
+    }
+    out[e] = v;
+}
+
+}  // namespace pn2
+
+using namespace pn2;
+
+extern "C" int pn2_index_points_f32(const float *pts, int64_t B, int64_t N, int64_t C,
+                                    int64_t sb, int64_t sn, int64_t sc, const int64_t *idx,
+                                    int64_t M, float *out, void *stream) {
+    PN2_REQUIRE(pts && idx && out, "pn2_index_points_f32: null pointer");
+    PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && M >= 0, "pn2_index_points_f32: bad shape");
+    const int64_t tot = B * M * C;
+    if (tot == 0) return PN2_OK;
+    hipLaunchKernelGGL(index_points_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), pts, B, N, C, sb, sn, sc, idx, M, out);
+    PN2_LAUNCH_CHECK("index_points_kernel");
+    return PN2_OK;
+}
+
+extern "C" int pn2_group_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,
+                             int64_t sn, int64_t sc, const float *feat, int64_t D, int64_t fb,
+                             int64_t fn, int64_t fd, const float *ctr, int64_t S,
+                             const int64_t *idx, int64_t K, int feature_first, float *out,
+                             void *stream) {
+    PN2_REQUIRE(pts && ctr && idx && out, "pn2_group_f32: null pointer");
+    PN2_REQUIRE(D == 0 || feat, "pn2_group_f32: D > 0 but feat is null");
+    PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && D >= 0 && S >= 0 && K >= 1,
+                "pn2_group_f32: bad shape");
+    const int64_t tot = B * S * K * (C + D);
+    if (tot == 0) return PN2_OK;
+    hipLaunchKernelGGL(group_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), pts, N, C, sb, sn, sc, feat, D, fb, fn, fd, ctr, S, idx,
+                       K, feature_first, tot, out);
+    PN2_LAUNCH_CHECK("group_kernel");
+    return PN2_OK;
+}

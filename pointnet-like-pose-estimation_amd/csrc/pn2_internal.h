@@ -1,0 +1,118 @@
+// pn2_internal.h -- shared host/device helpers for libpn2.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "pn2.h"
+
+namespace pn2 {
+
+// ---------------------------------------------------------------- host-side error plumbing
+int set_error(int code, const char *fmt, ...);
+
+#define PN2_REQUIRE(cond, ...)                                   \
+    do {                                                         \
+        if (!(cond)) return ::pn2::set_error(PN2_EINVAL, __VA_ARGS__); \
+    } while (0)
+
+#define PN2_LAUNCH_CHECK(what)                                                        \
+    do {                                                                              \
+        hipError_t e_ = hipGetLastError();                                            \
+        if (e_ != hipSuccess)                                                         \
+            return ::pn2::set_error(PN2_EHIP, "%s: %s", what, hipGetErrorString(e_)); \
+    } while (0)
+
+static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kMaxC = 16;  // point dims (xyz + one-hot) held in registers
+
+// --------------------------------------------------------------- device: reference sum orders
+// torch.sum(x**2, -1) over the channel axis, reproduced bit-for-bit (torch 2.10 CPU, AVX512);
+// pinned in oracle/pn2_oracle.c and tests/test_oracle_golden.py.
+//  contig  (stride_c == 1):  C<8 -> row_sum with 4 accumulators; C>=8 -> 8 lane partials,
+//                            scalar tail first, then tail+v0+...+v7.
+//  strided (stride_n == 1):  n < 16*floor(N/16) -> sequential; tail -> row_sum order.
+// `a` is a register array; C is runtime (<= CM).
+template <int CM>
+__device__ __forceinline__ float seq_sum(const float (&a)[CM], int C) {
+    float r = 0.f;
+#pragma unroll
+    for (int k = 0; k < CM; ++k)
+        if (k < C) r = __fadd_rn(r, a[k]);
+    return r;
+}
+
+template <int CM>
+__device__ __forceinline__ float rowsum4(const float (&a)[CM], int C) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int n4 = (C / 4) * 4;
+#pragma unroll
+    for (int k = 0; k < CM; ++k) {
+        if (k < n4) acc[k & 3] = __fadd_rn(acc[k & 3], a[k]);
+        else if (k < C) acc[0] = __fadd_rn(acc[0], a[k]);
+    }
+    return __fadd_rn(__fadd_rn(__fadd_rn(acc[0], acc[1]), acc[2]), acc[3]);
+}
+
+template <int CM>
+__device__ __forceinline__ float contig_sum(const float (&a)[CM], int C) {
+    if (C < 8) return rowsum4<CM>(a, C);
+    const int nv8 = (C / 8) * 8;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = 0.f;
+#pragma unroll
+    for (int k = 0; k < CM; ++k)
+        if (k < nv8) v[k & 7] = __fadd_rn(v[k & 7], a[k]);
+    float r = 0.f;
+#pragma unroll
+    for (int k = 0; k < CM; ++k)
+        if (k >= nv8 && k < C) r = __fadd_rn(r, a[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r = __fadd_rn(r, v[k]);
+    return r;
+}
+
+// rule: 0 = contig, 1 = strided sequential region, 2 = strided tail (row_sum)
+template <int CM>
+__device__ __forceinline__ float layout_sum(const float (&a)[CM], int C, int rule) {
+    if (rule == 0) return contig_sum<CM>(a, C);
+    if (rule == 1) return seq_sum<CM>(a, C);
+    return rowsum4<CM>(a, C);
+}
+
+__host__ __device__ __forceinline__ int layout_kind(int64_t sn, int64_t sc) {
+    return (sc != 1 && sn == 1) ? 1 : 0;  // 1: point-contiguous ("strided") rows
+}
+
+__device__ __forceinline__ int point_rule(int kind, int64_t n, int64_t N) {
+    if (kind == 0) return 0;
+    return (n < (N / 16) * 16) ? 1 : 2;
+}
+
+// ----------------------------------------------------------------- device: wave reductions
+// DPP row reductions: after these four steps every lane of a 16-lane row holds the row result.
+// (quad_perm xor1 = 0xB1, xor2 = 0x4E, row_half_mirror = 0x141, row_mirror = 0x140)
+#define PN2_DPP(v, ctrl) \
+    static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), ctrl, 0xF, 0xF, false))
+
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+    v = max(v, PN2_DPP(v, 0xB1));
+    v = max(v, PN2_DPP(v, 0x4E));
+    v = max(v, PN2_DPP(v, 0x141));
+    v = max(v, PN2_DPP(v, 0x140));
+    unsigned a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    unsigned c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return max(max(a, b), max(c, d));
+}
+
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+    // min via bitwise-not max (update_dpp's `old`=0 only matters for masked lanes; none here)
+    return ~wave_max_u32(~v);
+}
+
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+}  // namespace pn2

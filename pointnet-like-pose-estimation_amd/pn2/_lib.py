@@ -1,0 +1,100 @@
+"""ctypes binding of libpn2.so (the C ABI declared in include/pn2.h).
+
+The library is built in-tree for gfx950 (``make -C pointnet-like-pose-estimation_amd/csrc`` or
+``__graft_entry__.build()``) and shares torch's HIP runtime: torch is imported first, so the
+dynamic loader resolves libpn2's ``libamdhip64.so.7`` to the copy torch already loaded (one
+HIP context, torch streams valid in both).
+
+There is no fallback: if the library is missing or fails to load, every op raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before libpn2.so: shared HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpn2.so")
+
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_vp = ctypes.c_void_p
+_dbl = ctypes.c_double
+
+
+class Pn2Error(RuntimeError):
+    """A libpn2 entry point returned an error code (message from pn2_last_error)."""
+
+
+class MlpLayer(ctypes.Structure):
+    _fields_ = [("wt", _vp), ("alpha", _vp), ("beta", _vp), ("cin", _i64), ("cout", _i64)]
+
+
+class SaSrc(ctypes.Structure):
+    _fields_ = [
+        ("mode", _int),
+        ("pts", _vp), ("pb", _i64), ("pn", _i64), ("pc", _i64),
+        ("feat", _vp), ("fb", _i64), ("fn", _i64),
+        ("ctr", _vp),
+        ("idx", _vp),
+        ("rows", _vp), ("rs", _i64),
+        ("B", _i64), ("N", _i64), ("C", _i64), ("D", _i64), ("S", _i64), ("K", _i64),
+    ]
+
+
+SRC_GROUP_XYZ_FIRST = 0
+SRC_GROUP_FEAT_FIRST = 1
+SRC_GROUP_ALL = 2
+SRC_ROWS = 3
+
+# name -> (restype, argtypes); every symbol include/pn2.h declares
+SIGNATURES = {
+    "pn2_abi_version": (_int, []),
+    "pn2_last_error": (ctypes.c_char_p, []),
+    "pn2_packed_stride": (_i64, [_i64]),
+    "pn2_fps_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "pn2_pack_points_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "pn2_ball_query_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp]),
+    "pn2_square_distance_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "pn2_index_points_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp]),
+    "pn2_group_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
+                             _vp, _i64, _vp, _i64, _int, _vp, _vp]),
+    "pn2_layer_cin_pad": (_i64, [_i64]),
+    "pn2_pack_layer_f32": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _dbl, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "pn2_sa_mlp_workspace_bytes": (_i64, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int]),
+    "pn2_sa_mlp_max_f32": (_int, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int, _int, _vp,
+                                  _i64, _vp, _i64, _vp]),
+}
+
+ABI_VERSION = 1
+_lib = None
+
+
+def load():
+    """Load libpn2.so (once).  Raises if it is missing or incompatible -- no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "pn2: %s is not built; run `make -C pointnet-like-pose-estimation_amd/csrc` "
+            "(or __graft_entry__.build())" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.pn2_abi_version() != ABI_VERSION:
+        raise ImportError("pn2: libpn2.so ABI %d != expected %d" % (L.pn2_abi_version(), ABI_VERSION))
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().pn2_last_error().decode(errors="replace")
+        raise Pn2Error("%s failed (code %d): %s" % (what, rc, msg))
+
+
+def stream_ptr(device):
+    """hipStream_t of torch's current stream on `device`, as an int for ctypes."""
+    return torch.cuda.current_stream(device).cuda_stream

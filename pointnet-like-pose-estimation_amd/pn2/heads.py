@@ -1,0 +1,179 @@
+"""Layer-config restatements of the reference's PointNet++ heads, built on pn2's SA modules.
+
+The reference heads import ``pointnet2_utils`` by bare name and run unchanged on the drop-in
+(see tests/test_gpu_reference_heads.py); the reference sources never travel to the GPU box, so
+the benchmark and the on-box parity tests build the same networks from these restatements.
+Submodules are created in the reference's order, so a ``torch.manual_seed`` before
+construction yields the identical parameters (pinned by a state_dict hash in the goldens) and
+the ``state_dict`` keys match the reference's checkpoints.
+
+  ClsSSG          /root/reference/model/pointnet2_cls_ssg.py:5-38
+  ClsMSG          /root/reference/model/pointnet2_cls_msg.py:5-38
+  RotationSSG     /root/reference/model/rotation_ssg.py:5-38
+  TranslationSSG  /root/reference/model/translation_ssg.py:5-44
+  RotationMSG     /root/reference/model/rotation_msg.py:5-38
+  TranslationMSG  /root/reference/model/translation_msg.py:5-44
+  SignSSG         /root/reference/model/sign_ssg.py:5-36 (with the missing `import torch`)
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .pointnet2_utils import PointNetSetAbstraction as SA
+from .pointnet2_utils import PointNetSetAbstractionMsg as SAMsg
+
+
+class _FCHead(nn.Module):
+    """fc1/bn1/relu/drop -> fc2/bn2/relu/drop -> fc3, shared by every head."""
+
+    def _fc(self, x):
+        x = self.drop(F.relu(self.bn1(self.fc1(x))))
+        x = self.drop(F.relu(self.bn2(self.fc2(x))))
+        return self.fc3(x)
+
+    def _make_fc(self, out):
+        self.fc1 = nn.Linear(1024, 512)
+        self.fc2 = nn.Linear(512, 256)
+        self.fc3 = nn.Linear(256, out)
+        self.drop = nn.Dropout(0.4)
+        self.bn1 = nn.BatchNorm1d(512)
+        self.bn2 = nn.BatchNorm1d(256)
+
+
+class ClsSSG(_FCHead):
+    def __init__(self, num_category=7):
+        super().__init__()
+        self.sa1 = SA(512, 32, 0.2, 3, [64, 64, 128], False)
+        self.sa2 = SA(128, 64, 0.4, 128 + 3, [128, 128, 256], False)
+        self.sa3 = SA(None, None, None, 256 + 3, [256, 512, 1024], True)
+        self._make_fc(num_category)
+
+    def forward(self, points):
+        B = points.shape[0]
+        l1p, l1f = self.sa1(points, None)
+        l2p, l2f = self.sa2(l1p, l1f)
+        _, l3f = self.sa3(l2p, l2f)
+        x = F.log_softmax(self._fc(l3f.reshape(B, 1024)), -1)
+        return x, l3f, x.data.max(1)[1]
+
+
+class ClsMSG(_FCHead):
+    def __init__(self, num_category=7):
+        super().__init__()
+        self.sa1 = SAMsg(512, [16, 32, 128], [0.1, 0.2, 0.4], 0, [[32, 32, 64], [64, 64, 128], [64, 96, 128]])
+        self.sa2 = SAMsg(128, [32, 64, 128], [0.2, 0.4, 0.8], 320, [[64, 64, 128], [128, 128, 256], [128, 128, 256]])
+        self.sa3 = SA(None, None, None, 640 + 3, [256, 512, 1024], True)
+        self._make_fc(num_category)
+
+    def forward(self, points):
+        B = points.shape[0]
+        l1p, l1f = self.sa1(points, None)
+        l2p, l2f = self.sa2(l1p, l1f)
+        _, l3f = self.sa3(l2p, l2f)
+        x = F.log_softmax(self._fc(l3f.reshape(B, 1024)), -1)
+        return x, l3f, x.data.max(1)[1]
+
+
+class RotationSSG(_FCHead):
+    def __init__(self, num_category=7):
+        super().__init__()
+        ch = 3 + num_category
+        self.sa1 = SA(512, 32, 0.2, ch, [64, 64, 128], False)
+        self.sa2 = SA(128, 64, 0.4, 128 + ch, [128, 128, 256], False)
+        self.sa3 = SA(None, None, None, 256 + ch, [256, 512, 1024], True)
+        self._make_fc(3)
+
+    def forward(self, points):
+        B = points.shape[0]
+        l1p, l1f = self.sa1(points, None)
+        l2p, l2f = self.sa2(l1p, l1f)
+        _, l3f = self.sa3(l2p, l2f)
+        return self._fc(l3f.reshape(B, 1024))
+
+
+class TranslationSSG(_FCHead):
+    def __init__(self, num_category=7, mean_mlp='True'):
+        super().__init__()
+        self.mean_mlp = mean_mlp
+        ch = 3 + num_category
+        self.sa1 = SA(512, 32, 0.2, ch, [64, 64, 128], False)
+        self.sa2 = SA(None, None, None, 128 + ch, [256, 512, 1024], True)
+        self._make_fc(3)
+        if mean_mlp == 'True':  # string compare, as the reference (translation_ssg.py:23)
+            self.mean_fc1 = nn.Linear(3, 6)
+            self.mean_fc2 = nn.Linear(6, 3)
+            self.mean_bn1 = nn.BatchNorm1d(6)
+
+    def forward(self, points, mean):
+        B = points.shape[0]
+        if self.mean_mlp == 'True':
+            mean = self.mean_fc2(F.relu(self.mean_bn1(self.mean_fc1(mean))))
+        l1p, l1f = self.sa1(points, None)
+        _, l2f = self.sa2(l1p, l1f)
+        return self._fc(l2f.reshape(B, 1024)) + mean
+
+
+class RotationMSG(_FCHead):
+    def __init__(self, num_category=7):
+        super().__init__()
+        ch = 3 + num_category
+        self.sa1 = SAMsg(512, [16, 32, 128], [0.1, 0.2, 0.4], 0, [[32, 32, 64], [64, 64, 128], [64, 96, 128]], num_category=num_category)
+        self.sa2 = SAMsg(128, [32, 64, 128], [0.2, 0.4, 0.8], 320, [[64, 64, 128], [128, 128, 256], [128, 128, 256]], num_category=num_category)
+        self.sa3 = SA(None, None, None, 640 + ch, [256, 512, 1024], True)
+        self._make_fc(3)
+
+    def forward(self, points):
+        B = points.shape[0]
+        l1p, l1f = self.sa1(points, None)
+        l2p, l2f = self.sa2(l1p, l1f)
+        _, l3f = self.sa3(l2p, l2f)
+        return self._fc(l3f.reshape(B, 1024))
+
+
+class TranslationMSG(_FCHead):
+    def __init__(self, num_category=7, mean_mlp='True'):
+        super().__init__()
+        self.mean_mlp = mean_mlp
+        ch = 3 + num_category
+        self.sa1 = SAMsg(512, [16, 32, 64], [0.1, 0.2, 0.4], 0, [[32, 64, 128], [64, 128, 256], [96, 128, 256]], num_category=num_category)
+        self.sa2 = SA(None, None, None, 640 + ch, [256, 512, 1024], True)
+        self._make_fc(3)
+        if mean_mlp == 'True':
+            self.mean_fc1 = nn.Linear(3, 6)
+            self.mean_fc2 = nn.Linear(6, 3)
+            self.mean_bn1 = nn.BatchNorm1d(6)
+
+    def forward(self, points, mean):
+        B = points.shape[0]
+        if self.mean_mlp == 'True':
+            mean = self.mean_fc2(F.relu(self.mean_bn1(self.mean_fc1(mean))))
+        l1p, l1f = self.sa1(points, None)
+        _, l2f = self.sa2(l1p, l1f)
+        return self._fc(l2f.reshape(B, 1024)) + mean
+
+
+class SignSSG(_FCHead):
+    def __init__(self, num_category=7):
+        super().__init__()
+        ch = 3 + num_category
+        self.sa1 = SA(512, 32, 0.2, ch, [64, 64, 128], False)
+        self.sa2 = SA(None, None, None, 128 + ch, [256, 512, 1024], True)
+        self._make_fc(1)
+
+    def forward(self, points):
+        B = points.shape[0]
+        l1p, l1f = self.sa1(points, None)
+        _, l2f = self.sa2(l1p, l1f)
+        x = torch.sigmoid(self._fc(l2f.reshape(B, 1024)))
+        return x, torch.sign(x - 0.5)
+
+
+HEADS = {
+    "pointnet2_cls_ssg": ClsSSG,
+    "pointnet2_cls_msg": ClsMSG,
+    "rotation_ssg": RotationSSG,
+    "translation_ssg": TranslationSSG,
+    "rotation_msg": RotationMSG,
+    "translation_msg": TranslationMSG,
+    "sign_ssg": SignSSG,
+}

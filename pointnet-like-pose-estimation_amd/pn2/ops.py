@@ -1,0 +1,277 @@
+"""PyTorch custom ops (namespace ``pn2``) over the libpn2.so C ABI.
+
+Each op takes/returns torch tensors, checks shapes in Python (raising the exception the
+reference raises for the same misuse), and calls the HIP entry point asynchronously on torch's
+current stream.  Device tensors only: there is no CPU implementation and no fallback -- a CPU
+tensor or a missing library is an error.
+
+Ops (reference code each replaces, in /root/reference/model/pointnet2_utils.py):
+  pn2::fps            farthest_point_sample :47-68 (+ index_points of the samples, :106)
+  pn2::pack_points    the torch.sum(points**2, -1) terms of square_distance :24-25
+  pn2::ball_query     query_ball_point :70-90
+  pn2::square_distance square_distance :5-26
+  pn2::index_points   index_points :28-45
+  pn2::group          grouping in sample_and_group :107-116 / the MSG module :204-209
+  pn2::pack_layer     Conv2d 1x1 + BatchNorm2d (eval) parameters :150-156, :184-193
+  pn2::sa_mlp_max_    gathered shared MLP + max :167-172, :211-218 (writes into `out`)
+"""
+from typing import List, Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+from ._lib import MlpLayer, SaSrc, check, load
+
+_L = load()  # fail at import, loudly, if the native library is unavailable
+
+
+def _dev(t: Tensor, what: str):
+    if t.device.type != "cuda":
+        raise RuntimeError("%s: pn2 runs on ROCm device tensors only (got %s); there is no CPU "
+                           "path" % (what, t.device))
+    if t.dtype != torch.float32 and t.dtype != torch.int64:
+        raise TypeError("%s: unsupported dtype %s" % (what, t.dtype))
+
+
+def _stream(t: Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def packed_stride(C: int) -> int:
+    return int(_L.pn2_packed_stride(C))
+
+
+def cin_pad(cin: int) -> int:
+    return int(_L.pn2_layer_cin_pad(cin))
+
+
+# ------------------------------------------------------------------------------ fps
+@torch.library.custom_op("pn2::fps", mutates_args=())
+def fps(points: Tensor, npoint: int, start: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """points [B,N,C] float32 (any strides), start [B] int64 -> (fps_idx [B,S] int64,
+    new_points [B,S,C], packed centroids [B,S,cp], packed points [B,N,cp])."""
+    _dev(points, "pn2::fps")
+    B, N, C = points.shape
+    cp = packed_stride(C)
+    start = start.to(device=points.device, dtype=torch.int64).contiguous()
+    idx = torch.empty(B, npoint, dtype=torch.int64, device=points.device)
+    newp = torch.empty(B, npoint, C, dtype=torch.float32, device=points.device)
+    cpk = torch.empty(B, npoint, cp, dtype=torch.float32, device=points.device)
+    ppk = torch.empty(B, N, cp, dtype=torch.float32, device=points.device)
+    sb, sn, sc = points.stride()
+    check(_L.pn2_fps_f32(points.data_ptr(), B, N, C, sb, sn, sc, start.data_ptr(), npoint,
+                         idx.data_ptr(), newp.data_ptr(), cpk.data_ptr(), ppk.data_ptr(),
+                         _stream(points)), "pn2_fps_f32")
+    return idx, newp, cpk, ppk
+
+
+@fps.register_fake
+def _(points, npoint, start):
+    B, N, C = points.shape
+    cp = packed_stride(C)
+    e = points.new_empty
+    return (e(B, npoint, dtype=torch.int64), e(B, npoint, C), e(B, npoint, cp), e(B, N, cp))
+
+
+# ------------------------------------------------------------------------------ pack_points
+@torch.library.custom_op("pn2::pack_points", mutates_args=())
+def pack_points(points: Tensor) -> Tensor:
+    """[B,N,C] (any strides) -> [B,N,cp] records (coords, ssq in the reference's order, pad)."""
+    _dev(points, "pn2::pack_points")
+    B, N, C = points.shape
+    out = torch.empty(B, N, packed_stride(C), dtype=torch.float32, device=points.device)
+    sb, sn, sc = points.stride()
+    check(_L.pn2_pack_points_f32(points.data_ptr(), B, N, C, sb, sn, sc, out.data_ptr(),
+                                 _stream(points)), "pn2_pack_points_f32")
+    return out
+
+
+@pack_points.register_fake
+def _(points):
+    B, N, C = points.shape
+    return points.new_empty(B, N, packed_stride(C))
+
+
+# ------------------------------------------------------------------------------ ball query
+@torch.library.custom_op("pn2::ball_query", mutates_args=())
+def ball_query(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, nsample: int) -> Tensor:
+    """Packed points [B,N,cp] and centroids [B,S,cp] -> group_idx [B,S,nsample] int64."""
+    _dev(pts_packed, "pn2::ball_query")
+    B, N, _ = pts_packed.shape
+    S = ctr_packed.shape[1]
+    if nsample > N:
+        # the reference's `group_idx[mask] = group_first[mask]` fails the same way (:89)
+        raise IndexError("query_ball_point: sample_number %d > number of points %d" % (nsample, N))
+    out = torch.empty(B, S, nsample, dtype=torch.int64, device=pts_packed.device)
+    check(_L.pn2_ball_query_f32(pts_packed.data_ptr(), ctr_packed.data_ptr(), B, N, S, C,
+                                float(radius), nsample, out.data_ptr(), _stream(pts_packed)),
+          "pn2_ball_query_f32")
+    return out
+
+
+@ball_query.register_fake
+def _(pts_packed, ctr_packed, C, radius, nsample):
+    return pts_packed.new_empty(pts_packed.shape[0], ctr_packed.shape[1], nsample, dtype=torch.int64)
+
+
+# ------------------------------------------------------------------------------ square_distance
+@torch.library.custom_op("pn2::square_distance", mutates_args=())
+def square_distance(src_packed: Tensor, dst_packed: Tensor, C: int) -> Tensor:
+    _dev(src_packed, "pn2::square_distance")
+    B, S, _ = src_packed.shape
+    N = dst_packed.shape[1]
+    out = torch.empty(B, S, N, dtype=torch.float32, device=src_packed.device)
+    check(_L.pn2_square_distance_f32(src_packed.data_ptr(), dst_packed.data_ptr(), B, S, N, C,
+                                     out.data_ptr(), _stream(src_packed)), "pn2_square_distance_f32")
+    return out
+
+
+@square_distance.register_fake
+def _(src_packed, dst_packed, C):
+    return src_packed.new_empty(src_packed.shape[0], src_packed.shape[1], dst_packed.shape[1])
+
+
+# ------------------------------------------------------------------------------ index_points
+@torch.library.custom_op("pn2::index_points", mutates_args=())
+def index_points(points: Tensor, idx: Tensor) -> Tensor:
+    """points [B,N,C] (any strides), idx [B,M] int64 -> [B,M,C] contiguous."""
+    _dev(points, "pn2::index_points")
+    B, N, C = points.shape
+    M = idx.shape[1]
+    idx = idx.contiguous()
+    out = torch.empty(B, M, C, dtype=torch.float32, device=points.device)
+    sb, sn, sc = points.stride()
+    check(_L.pn2_index_points_f32(points.data_ptr(), B, N, C, sb, sn, sc, idx.data_ptr(), M,
+                                  out.data_ptr(), _stream(points)), "pn2_index_points_f32")
+    return out
+
+
+@index_points.register_fake
+def _(points, idx):
+    return points.new_empty(points.shape[0], idx.shape[1], points.shape[2])
+
+
+# ------------------------------------------------------------------------------ group
+@torch.library.custom_op("pn2::group", mutates_args=())
+def group(points: Tensor, feature: Optional[Tensor], centers: Tensor, idx: Tensor,
+          feature_first: bool) -> Tensor:
+    """[B,S,K,C+D]: [xyz(idx) - centre, feature(idx)] (or feature first, the MSG order)."""
+    _dev(points, "pn2::group")
+    B, N, C = points.shape
+    S, K = idx.shape[1], idx.shape[2]
+    D = 0 if feature is None else feature.shape[2]
+    centers = centers.contiguous()
+    idx = idx.contiguous()
+    out = torch.empty(B, S, K, C + D, dtype=torch.float32, device=points.device)
+    sb, sn, sc = points.stride()
+    if feature is None:
+        fp, fb, fn, fd = 0, 0, 0, 0
+    else:
+        fp = feature.data_ptr()
+        fb, fn, fd = feature.stride()
+    check(_L.pn2_group_f32(points.data_ptr(), B, N, C, sb, sn, sc, fp, D, fb, fn, fd,
+                           centers.data_ptr(), S, idx.data_ptr(), K, int(feature_first),
+                           out.data_ptr(), _stream(points)), "pn2_group_f32")
+    return out
+
+
+@group.register_fake
+def _(points, feature, centers, idx, feature_first):
+    D = 0 if feature is None else feature.shape[2]
+    return points.new_empty(points.shape[0], idx.shape[1], idx.shape[2], points.shape[2] + D)
+
+
+# ------------------------------------------------------------------------------ pack_layer
+@torch.library.custom_op("pn2::pack_layer", mutates_args=())
+def pack_layer(weight: Tensor, bias: Optional[Tensor], gamma: Optional[Tensor],
+               beta: Optional[Tensor], mean: Optional[Tensor], var: Optional[Tensor],
+               eps: float) -> Tuple[Tensor, Tensor, Tensor]:
+    """Conv2d 1x1 weight [cout,cin,1,1] (+ bias) and eval BatchNorm2d stats -> (W^T padded
+    [cin_pad,cout], alpha [cout], beta [cout]) with layer(x) = relu(alpha*(W x) + beta)."""
+    _dev(weight, "pn2::pack_layer")
+    cout, cin = weight.shape[0], weight.shape[1]
+    w = weight.reshape(cout, cin).contiguous()
+    dev = weight.device
+    wt = torch.empty(cin_pad(cin), cout, dtype=torch.float32, device=dev)
+    al = torch.empty(cout, dtype=torch.float32, device=dev)
+    be = torch.empty(cout, dtype=torch.float32, device=dev)
+
+    def p(t):
+        return 0 if t is None else t.contiguous().data_ptr()
+    keep = [None if t is None else t.contiguous() for t in (bias, gamma, beta, mean, var)]
+    check(_L.pn2_pack_layer_f32(w.data_ptr(), *[p(t) for t in keep], float(eps), cout, cin,
+                                wt.data_ptr(), al.data_ptr(), be.data_ptr(), _stream(weight)),
+          "pn2_pack_layer_f32")
+    return wt, al, be
+
+
+@pack_layer.register_fake
+def _(weight, bias, gamma, beta, mean, var, eps):
+    cout, cin = weight.shape[0], weight.shape[1]
+    e = weight.new_empty
+    return e(cin_pad(cin), cout), e(cout), e(cout)
+
+
+# ------------------------------------------------------------------------------ sa_mlp_max_
+def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K):
+    s = SaSrc()
+    s.mode = mode
+    if points is not None:
+        s.pts = points.data_ptr()
+        s.pb, s.pn, s.pc = points.stride()
+    if feature is not None:
+        if feature.stride(2) != 1:
+            raise ValueError("pn2::sa_mlp_max_: features must be channels-last (stride 1)")
+        s.feat = feature.data_ptr()
+        s.fb, s.fn = feature.stride(0), feature.stride(1)
+    if centers is not None:
+        s.ctr = centers.data_ptr()
+    if idx is not None:
+        s.idx = idx.data_ptr()
+    if rows is not None:
+        s.rows = rows.data_ptr()
+        s.rs = rows.stride(0)
+    s.B, s.N, s.C, s.D, s.S, s.K = B, N, C, D, S, K
+    return s
+
+
+@torch.library.custom_op("pn2::sa_mlp_max_", mutates_args=("out",))
+def sa_mlp_max_(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor],
+                centers: Optional[Tensor], idx: Optional[Tensor], wts: List[Tensor],
+                alphas: List[Tensor], betas: List[Tensor], cins: List[int]) -> None:
+    """Fused gather -> MLP (conv1x1+BN+ReLU)* -> max over each group, written channels-last
+    into `out` ([G, >=cout] view with unit column stride; G = B*S groups, or B for
+    group_all).  mode: 0 SSG grouping, 1 MSG grouping, 2 group_all."""
+    _dev(points, "pn2::sa_mlp_max_")
+    B, N, C = points.shape
+    D = 0 if feature is None else feature.shape[2]
+    if mode == _lib.SRC_GROUP_ALL:
+        S, K = 1, N
+    else:
+        S, K = idx.shape[1], idx.shape[2]
+        idx = idx.contiguous()
+        centers = centers.contiguous()
+    src = _src(mode, points, feature, centers, idx, None, B, N, C, D, S, K)
+    n = len(wts)
+    layers = (MlpLayer * n)()
+    for i in range(n):
+        layers[i].wt = wts[i].data_ptr()
+        layers[i].alpha = alphas[i].data_ptr()
+        layers[i].beta = betas[i].data_ptr()
+        layers[i].cin = cins[i]
+        layers[i].cout = wts[i].shape[1]
+    if out.stride(-1) != 1:
+        raise ValueError("pn2::sa_mlp_max_: out must have unit column stride")
+    ws_bytes = int(_L.pn2_sa_mlp_workspace_bytes(src, layers, n))
+    if ws_bytes < 0:
+        check(-1, "pn2_sa_mlp_workspace_bytes")
+    ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=points.device) if ws_bytes else None
+    check(_L.pn2_sa_mlp_max_f32(src, layers, n, 1, out.data_ptr(), out.stride(-2),
+                                0 if ws is None else ws.data_ptr(), ws_bytes, _stream(points)),
+          "pn2_sa_mlp_max_f32")
+
+
+@sa_mlp_max_.register_fake
+def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins):
+    return None

@@ -1,0 +1,263 @@
+"""Drop-in replacement for /root/reference/model/pointnet2_utils.py on MI355X.
+
+Same public names, signatures, return shapes, ``state_dict`` keys and CPU-RNG consumption as
+the reference, so its heads (pointnet2_cls_ssg/msg, rotation_/translation_/sign_*) run
+unchanged when this module is importable as ``pointnet2_utils`` (see the shim
+``pointnet-like-pose-estimation_amd/pointnet2_utils.py``).
+
+Eval-mode inference (``model.eval()`` / no autograd) of an SA layer is three HIP launches:
+  pn2::fps            FPS + gathered centroids + packed (coords, ssq) records
+  pn2::ball_query     first-K-in-radius neighbour indices
+  pn2::sa_mlp_max_    fused gather -> conv1x1/BN/ReLU chain -> max over neighbours
+(+ per scale for the MSG module).  Hidden activations never leave LDS; the per-layer
+``[B, C, K, S]`` tensors of the reference are never materialised.
+
+Training (``model.train()`` or autograd through the weights) keeps the reference's semantics
+(batch-statistics BatchNorm, autograd through the MLP and the feature gather): FPS and the ball
+query still run as HIP kernels (they are index ops with no gradient), the differentiable part
+runs as torch device ops.
+
+Device tensors only -- the reference's CPU execution is not re-implemented here.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from . import ops
+from . import shard
+
+
+# ----------------------------------------------------------------------------- helpers
+def _draw_start(B, N, device):
+    """The reference's FPS start draw: torch.randint(0, N, (B,), dtype=long) on the CPU default
+    generator (pointnet2_utils.py:59) -- one draw per FPS call, sliced when sharded."""
+    return shard.draw_start(B, N).to(device, non_blocking=True)
+
+
+def _channels_last(feature):
+    """[B, D, N] feature -> a [B, N, D] view with unit channel stride (copy only if needed)."""
+    f = feature.permute(0, 2, 1)
+    return f if f.stride(2) == 1 else f.contiguous()
+
+
+def _needs_autograd(module, *tensors):
+    if module.training:
+        return True
+    if not torch.is_grad_enabled():
+        return False
+    return any(p.requires_grad for p in module.parameters()) or any(
+        t is not None and t.requires_grad for t in tensors)
+
+
+def _pack_chain(convs, bns, cache):
+    """Fold each Conv2d-1x1 + eval BatchNorm2d into (W^T, alpha, beta); cached until any
+    parameter/buffer changes (data_ptr or in-place version)."""
+    tensors = []
+    for conv, bn in zip(convs, bns):
+        tensors += [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+    key = tuple((None if t is None else (t.data_ptr(), t._version)) for t in tensors)
+    if cache.get("key") != key:
+        wts, als, bes, cins = [], [], [], []
+        with torch.no_grad():
+            for conv, bn in zip(convs, bns):
+                wt, al, be = ops.pack_layer(conv.weight, conv.bias, bn.weight, bn.bias,
+                                            bn.running_mean, bn.running_var, float(bn.eps))
+                wts.append(wt)
+                als.append(al)
+                bes.append(be)
+                cins.append(conv.weight.shape[1])
+        cache["key"] = key
+        cache["layers"] = (wts, als, bes, cins)
+    return cache["layers"]
+
+
+def _torch_group(points, idx, centers, feature, feature_first):
+    """Differentiable grouping for the training path (torch device gathers)."""
+    B = points.shape[0]
+    b = torch.arange(B, device=points.device).view(B, 1, 1)
+    g = points[b, idx, :] - centers.unsqueeze(2)
+    if feature is None:
+        return g
+    f = feature[b, idx, :]
+    return torch.cat([f, g] if feature_first else [g, f], dim=-1)
+
+
+def _torch_mlp_max(grouped, convs, bns):
+    x = grouped.permute(0, 3, 2, 1)  # [B, C, K, S] as the reference (:167)
+    for conv, bn in zip(convs, bns):
+        x = F.relu(bn(conv(x)))
+    return torch.max(x, 2)[0]
+
+
+# ----------------------------------------------------------------------------- public functions
+def square_distance(src, dst):
+    """pointnet2_utils.py:5-26 -> [B, N, M], bit-identical to the reference's float32 result."""
+    C = src.shape[-1]
+    return ops.square_distance(ops.pack_points(src), ops.pack_points(dst), C)
+
+
+def index_points(points, idx):
+    """pointnet2_utils.py:28-45: points [B,N,C], idx [B, ...] -> [B, ..., C]."""
+    B = points.shape[0]
+    out = ops.index_points(points, idx.reshape(B, -1))
+    return out.view(*idx.shape, points.shape[-1])
+
+
+def farthest_point_sample(points, number):
+    """pointnet2_utils.py:47-68: [B,N,C] -> [B, number] int64 (consumes one CPU randint)."""
+    B, N, _ = points.shape
+    return ops.fps(points, number, _draw_start(B, N, points.device))[0]
+
+
+def query_ball_point(radius, number, points, new_points):
+    """pointnet2_utils.py:70-90: [B,S,number] int64; IndexError if number > N (as the
+    reference)."""
+    C = points.shape[-1]
+    return ops.ball_query(ops.pack_points(points), ops.pack_points(new_points), C, radius, number)
+
+
+def sample_and_group(points, feature, point_number, sample_number, radius, returnfps=False):
+    """pointnet2_utils.py:92-120.  points [B,N,C], feature [B,N,D] or None."""
+    B, N, C = points.shape
+    fps_idx, new_points, cpk, ppk = ops.fps(points, point_number, _draw_start(B, N, points.device))
+    idx = ops.ball_query(ppk, cpk, C, radius, sample_number)
+    new_feature = ops.group(points, feature, new_points, idx, False)
+    if returnfps:
+        grouped = index_points(feature if feature is not None else points, idx)
+        return new_points, new_feature, grouped, fps_idx
+    return new_points, new_feature
+
+
+def sample_and_group_all(points, feature):
+    """pointnet2_utils.py:122-141: centroid at the origin, raw xyz (not centred) first."""
+    B, N, C = points.shape
+    new_points = torch.zeros(B, 1, C, device=points.device, dtype=points.dtype)
+    grouped = points.reshape(B, 1, N, C)
+    if feature is not None:
+        return new_points, torch.cat([grouped, feature.reshape(B, 1, N, -1)], dim=-1)
+    return new_points, grouped
+
+
+# ----------------------------------------------------------------------------- modules
+class PointNetSetAbstraction(nn.Module):
+    """pointnet2_utils.py:143-174 (same ctor, submodule names and forward contract)."""
+
+    def __init__(self, point_number, sample_number, radius, in_channel, mlp, group_all=False):
+        super(PointNetSetAbstraction, self).__init__()
+        self.point_number = point_number
+        self.radius = radius
+        self.sample_number = sample_number
+        self.group_all = group_all
+        self.mlp_convs = nn.ModuleList()
+        self.mlp_bns = nn.ModuleList()
+        last = in_channel
+        for out_channel in mlp:
+            self.mlp_convs.append(nn.Conv2d(last, out_channel, 1))
+            self.mlp_bns.append(nn.BatchNorm2d(out_channel))
+            last = out_channel
+        self._pack_cache = {}
+
+    def forward(self, points, feature):
+        """points [B,C,N], feature [B,D,N] or None -> (new_points [B,C,S], new_feature
+        [B,mlp[-1],S]).  Both outputs are channel-first views of channels-last buffers."""
+        if _needs_autograd(self, points, feature):
+            return self._forward_autograd(points, feature)
+        pts = points.permute(0, 2, 1)
+        feat = None if feature is None else _channels_last(feature)
+        B, N, C = pts.shape
+        wts, als, bes, cins = _pack_chain(self.mlp_convs, self.mlp_bns, self._pack_cache)
+        cout = wts[-1].shape[1]
+        dev = pts.device
+        if self.group_all:
+            out = torch.empty(B, cout, device=dev, dtype=torch.float32)
+            ops.sa_mlp_max_(out, _lib.SRC_GROUP_ALL, pts, feat, None, None, wts, als, bes, cins)
+            new_points = torch.zeros(B, C, 1, device=dev, dtype=torch.float32)
+            return new_points, out.view(B, 1, cout).permute(0, 2, 1)
+        S, K = self.point_number, self.sample_number
+        _, new_points, cpk, ppk = ops.fps(pts, S, _draw_start(B, N, dev))
+        idx = ops.ball_query(ppk, cpk, C, self.radius, K)
+        out = torch.empty(B * S, cout, device=dev, dtype=torch.float32)
+        ops.sa_mlp_max_(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
+                        cins)
+        return new_points.permute(0, 2, 1), out.view(B, S, cout).permute(0, 2, 1)
+
+    def _forward_autograd(self, points, feature):
+        pts = points.permute(0, 2, 1)
+        feat = None if feature is None else feature.permute(0, 2, 1)
+        if self.group_all:
+            new_points, grouped = sample_and_group_all(pts, feat)
+        else:
+            B, N, C = pts.shape
+            _, new_points, cpk, ppk = ops.fps(pts.detach(), self.point_number,
+                                              _draw_start(B, N, pts.device))
+            idx = ops.ball_query(ppk, cpk, C, self.radius, self.sample_number)
+            grouped = _torch_group(pts, idx, new_points, feat, False)
+        return new_points.permute(0, 2, 1), _torch_mlp_max(grouped, self.mlp_convs, self.mlp_bns)
+
+
+class PointNetSetAbstractionMsg(nn.Module):
+    """pointnet2_utils.py:176-223 (same ctor, submodule names and forward contract)."""
+
+    def __init__(self, point_number, sample_number_list, radius_list, in_channel, mlp_list,
+                 num_category=0):
+        super(PointNetSetAbstractionMsg, self).__init__()
+        self.point_number = point_number
+        self.radius_list = radius_list
+        self.sample_number_list = sample_number_list
+        self.conv_blocks = nn.ModuleList()
+        self.bn_blocks = nn.ModuleList()
+        for widths in mlp_list:
+            convs = nn.ModuleList()
+            bns = nn.ModuleList()
+            last = in_channel + 3 + num_category
+            for out_channel in widths:
+                convs.append(nn.Conv2d(last, out_channel, 1))
+                bns.append(nn.BatchNorm2d(out_channel))
+                last = out_channel
+            self.conv_blocks.append(convs)
+            self.bn_blocks.append(bns)
+        self._pack_cache = [{} for _ in mlp_list]
+
+    def forward(self, points, feature):
+        if _needs_autograd(self, points, feature):
+            return self._forward_autograd(points, feature)
+        pts = points.permute(0, 2, 1)
+        feat = None if feature is None else _channels_last(feature)
+        B, N, C = pts.shape
+        S = self.point_number
+        dev = pts.device
+        chains = [_pack_chain(self.conv_blocks[i], self.bn_blocks[i], self._pack_cache[i])
+                  for i in range(len(self.radius_list))]
+        total = sum(ch[0][-1].shape[1] for ch in chains)
+        _, new_points, cpk, ppk = ops.fps(pts, S, _draw_start(B, N, dev))
+        out = torch.empty(B * S, total, device=dev, dtype=torch.float32)
+        col = 0
+        for i, radius in enumerate(self.radius_list):
+            wts, als, bes, cins = chains[i]
+            cout = wts[-1].shape[1]
+            idx = ops.ball_query(ppk, cpk, C, radius, self.sample_number_list[i])
+            ops.sa_mlp_max_(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
+                            new_points, idx, wts, als, bes, cins)
+            col += cout
+        return new_points.permute(0, 2, 1), out.view(B, S, total).permute(0, 2, 1)
+
+    def _forward_autograd(self, points, feature):
+        pts = points.permute(0, 2, 1)
+        feat = None if feature is None else feature.permute(0, 2, 1)
+        B, N, C = pts.shape
+        _, new_points, cpk, ppk = ops.fps(pts.detach(), self.point_number,
+                                          _draw_start(B, N, pts.device))
+        outs = []
+        for i, radius in enumerate(self.radius_list):
+            idx = ops.ball_query(ppk, cpk, C, radius, self.sample_number_list[i])
+            grouped = _torch_group(pts, idx, new_points, feat, True)
+            outs.append(_torch_mlp_max(grouped, self.conv_blocks[i], self.bn_blocks[i]))
+        return new_points.permute(0, 2, 1), torch.cat(outs, dim=1)
+
+
+__all__ = [
+    "square_distance", "index_points", "farthest_point_sample", "query_ball_point",
+    "sample_and_group", "sample_and_group_all", "PointNetSetAbstraction",
+    "PointNetSetAbstractionMsg",
+]

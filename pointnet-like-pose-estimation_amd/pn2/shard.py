@@ -1,0 +1,67 @@
+"""Batch sharding across GPUs (one process per GPU, RCCL over xGMI).
+
+Every cloud of an eval-mode PointNet++ forward is independent (BatchNorm uses running stats,
+FPS / ball query / grouping are per cloud), so a global batch splits into contiguous per-rank
+shards with no exchange inside the forward.  Two things keep the sharded run identical to the
+single-GPU run of the whole batch:
+
+  * FPS start indices.  The reference draws ``torch.randint(0, N, (B,))`` from the CPU default
+    generator once per SA layer (pointnet2_utils.py:59).  Inside ``batch_shard(global_B,
+    offset)`` every rank draws the FULL-batch vector (same seed -> same stream on every rank)
+    and keeps its slice, so the RNG stream advances exactly as in the unsharded run.
+  * The only collective: ``all_gather_rows`` of the per-rank head outputs (logits, [B/W, k]
+    fp32 -- a few hundred bytes, latency-bound over xGMI).
+"""
+import contextlib
+import threading
+
+import torch
+import torch.distributed as dist
+
+_state = threading.local()
+
+
+@contextlib.contextmanager
+def batch_shard(global_batch, offset):
+    """Within this context FPS start draws are taken for `global_batch` clouds and sliced at
+    `offset` (this rank's first cloud)."""
+    prev = getattr(_state, "spec", None)
+    _state.spec = (int(global_batch), int(offset))
+    try:
+        yield
+    finally:
+        _state.spec = prev
+
+
+def draw_start(B, N):
+    """CPU int64 [B]: the reference's randint draw (or this shard's slice of it), pinned so the
+    host->device copy is asynchronous."""
+    spec = getattr(_state, "spec", None)
+    if spec is None:
+        t = torch.randint(0, N, (B,), dtype=torch.long)
+    else:
+        gb, off = spec
+        if off + B > gb:
+            raise ValueError("batch_shard: shard [%d, %d) outside global batch %d" % (off, off + B, gb))
+        t = torch.randint(0, N, (gb,), dtype=torch.long)[off:off + B]
+    return t.pin_memory() if torch.cuda.is_available() else t
+
+
+def shard_range(global_batch, rank, world):
+    """Contiguous [lo, hi) of clouds owned by `rank` (the remainder goes to the first ranks)."""
+    base, rem = divmod(global_batch, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def all_gather_rows(local, group=None):
+    """Concatenate every rank's [b_r, ...] tensor along dim 0 (equal b_r; RCCL all_gather on
+    GPU tensors, gloo on CPU ones)."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return local
+    local = local.contiguous()
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    dist.all_gather_into_tensor(out, local, group=group)
+    return out

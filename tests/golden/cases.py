@@ -1,0 +1,103 @@
+"""Deterministic inputs shared by the golden generator (make_goldens.py, run in the survey
+container against the imported reference) and the tests (run anywhere, incl. the GPU box).
+
+Everything is derived from seeds with torch's CPU generators, so the same torch version
+regenerates the same tensors; the goldens also store the inputs, and tests check both.
+"""
+import hashlib
+
+import numpy as np
+import torch
+
+
+def cloud(kind, B, N, seed, labels=None):
+    """A [B, N, C] float32 cloud (contiguous), unit-sphere normalised like provider.normalization
+    (/root/reference/provider.py:5-21).  kind:
+      'uniform3'  U[-1,1)^3
+      'dup3'      uniform, then provider.random_point_dropout-style duplication of point 0
+                  (/root/reference/provider.py:157-164): many exact duplicates -> FPS ties
+      'onehot10'  xyz + 7-way one-hot of `labels` (provider.splice_torch, provider.py:166-180)
+      'randn10'   N(0,1) in all 10 channels (not a real input; pins the channel-sum order)
+    """
+    g = torch.Generator().manual_seed(seed)
+    if kind == 'randn10':
+        return torch.randn(B, N, 10, generator=g)
+    xyz = torch.rand(B, N, 3, generator=g) * 2 - 1
+    if kind == 'dup3':
+        for b in range(B):
+            ratio = float(torch.rand(1, generator=g)) * 0.875
+            drop = torch.rand(N, generator=g) <= ratio
+            xyz[b, drop] = xyz[b, 0].clone()
+    xyz = xyz - xyz.mean(1, keepdim=True)
+    xyz = xyz / xyz.norm(dim=2).max(1)[0].view(B, 1, 1)
+    if kind in ('uniform3', 'dup3'):
+        return xyz.contiguous()
+    if kind == 'onehot10':
+        if labels is None:
+            labels = torch.arange(B) % 7
+        oh = torch.zeros(B, N, 7)
+        oh[torch.arange(B), :, labels] = 1.0
+        return torch.cat([xyz, oh], 2).contiguous()
+    raise ValueError(kind)
+
+
+def as_layout(pts_bnc, layout):
+    """[B,N,C] view with the requested storage: 'contig' ([B,N,C] storage) or 'strided'
+    ([B,C,N] storage, i.e. the permute(0,2,1) of the reference's model input)."""
+    if layout == 'contig':
+        return pts_bnc.contiguous()
+    return pts_bnc.permute(0, 2, 1).contiguous().permute(0, 2, 1)
+
+
+def randomize_bn(model, seed):
+    """Non-trivial eval-mode BatchNorm statistics/affine, in module order."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for m in model.modules():
+            if isinstance(m, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
+                n = m.num_features
+                m.running_mean.copy_(torch.rand(n, generator=g) * 0.2 - 0.1)
+                m.running_var.copy_(torch.rand(n, generator=g) + 0.5)
+                m.weight.copy_(torch.rand(n, generator=g) + 0.5)
+                m.bias.copy_(torch.rand(n, generator=g) * 0.2 - 0.1)
+
+
+def build_head(factory, w_seed, **kw):
+    torch.manual_seed(w_seed)
+    model = factory(**kw)
+    randomize_bn(model, w_seed + 1)
+    return model.eval()
+
+
+def state_hash(model):
+    h = hashlib.sha256()
+    for k, v in sorted(model.state_dict().items()):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(v.detach().cpu().numpy()).tobytes())
+    return h.hexdigest()
+
+
+# ----------------------------------------------------------------------- case tables
+# op-level index cases: name -> (kind, B, N, layout, S, [(radius, K), ...], seed)
+INDEX_CASES = {
+    'u3_strided':   ('uniform3', 4, 1024, 'strided', 512, [(0.2, 32), (0.4, 64), (0.1, 16), (0.8, 128)], 11),
+    'u3_contig':    ('uniform3', 3, 512, 'contig', 128, [(0.4, 64), (0.2, 32), (0.8, 128)], 12),
+    'dup3_strided': ('dup3', 4, 1024, 'strided', 512, [(0.2, 32), (0.4, 64)], 13),
+    'oh10_strided': ('onehot10', 7, 1024, 'strided', 512, [(0.2, 32), (0.1, 16), (0.4, 128)], 14),
+    'oh10_contig':  ('onehot10', 7, 512, 'contig', 128, [(0.4, 64), (0.8, 128)], 15),
+    'r10_contig':   ('randn10', 2, 1000, 'contig', 256, [(2.0, 32), (3.0, 64)], 16),
+    'r10_strided':  ('randn10', 2, 1000, 'strided', 256, [(2.0, 32), (3.0, 64)], 17),
+    'small_smoke':  ('uniform3', 2, 100, 'strided', 512, [(0.2, 32), (0.9, 100)], 18),
+    'tiny':         ('uniform3', 1, 10, 'contig', 4, [(0.5, 2), (2.0, 10)], 19),
+    'pose2048':     ('onehot10', 2, 2048, 'strided', 512, [(0.2, 32)], 20),
+    'stress16k':    ('uniform3', 1, 16384, 'strided', 512, [(0.2, 32)], 21),
+}
+
+# head-level cases: name -> (head, B, N, cloud kind, weight seed, forward seed)
+HEAD_CASES = {
+    'cls_ssg': ('pointnet2_cls_ssg', 2, 1024, 'uniform3', 100, 200),
+    'cls_msg': ('pointnet2_cls_msg', 2, 1024, 'uniform3', 101, 201),
+    'rotation_ssg': ('rotation_ssg', 2, 1024, 'onehot10', 102, 202),
+    'translation_ssg': ('translation_ssg', 2, 1024, 'onehot10', 103, 203),
+    'rotation_msg': ('rotation_msg', 2, 1024, 'onehot10', 104, 204),
+}

@@ -1,0 +1,115 @@
+"""Generate the golden fixtures by running the REFERENCE (PyTorch-CPU) implementation.
+
+Run only in the survey/build container, where /root/reference exists:
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_goldens.py
+It imports /root/reference/model/pointnet2_utils.py and the head modules read-only (no .pyc
+writes) and stores inputs + the reference's outputs as .npz data under tests/golden/.
+Nothing from the reference is copied: the fixtures are data only.
+
+Files:
+  index_<case>.npz  FPS indices / gathered centroids / ball-query indices / (small) square
+                    distance matrices, for the cases in cases.INDEX_CASES
+  head_<case>.npz   per-SA-layer outputs and head outputs for cases.HEAD_CASES (eval mode,
+                    seeded weights + BN statistics; the weights are regenerated from the seed
+                    and pinned by a state_dict SHA-256)
+  meta.json         torch version, CPU capability, MKL/oneDNN versions, thread count
+"""
+import json
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+REF_MODEL = "/root/reference/model"
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import cases  # noqa: E402
+
+
+def _ref():
+    if REF_MODEL not in sys.path:
+        sys.path.insert(0, REF_MODEL)
+    import importlib
+    return importlib.import_module("pointnet2_utils"), importlib
+
+
+def gen_index(P):
+    for name, (kind, B, N, layout, S, bqs, seed) in cases.INDEX_CASES.items():
+        pts = cases.as_layout(cases.cloud(kind, B, N, seed), layout)
+        torch.manual_seed(seed + 1000)
+        start = torch.randint(0, N, (B,), dtype=torch.long)
+        torch.manual_seed(seed + 1000)
+        fps_idx = P.farthest_point_sample(pts, S)  # draws the same start
+        new_points = P.index_points(pts, fps_idx)
+        rec = dict(points=pts.contiguous().numpy(), layout=np.array(layout), start=start.numpy(),
+                   S=np.array(S), fps_idx=fps_idx.numpy().astype(np.int32),
+                   new_points=new_points.numpy())
+        for i, (r, K) in enumerate(bqs):
+            try:
+                g = P.query_ball_point(r, K, pts, new_points).numpy().astype(np.int32)
+            except IndexError:
+                g = np.full((0,), -1, np.int32)  # reference raises: K > N
+            rec["bq%d_radius" % i] = np.array(r)
+            rec["bq%d_K" % i] = np.array(K)
+            rec["bq%d_idx" % i] = g
+        if B * S * N <= 110_000:
+            rec["sqdist"] = P.square_distance(new_points, pts).numpy()
+        np.savez_compressed(os.path.join(HERE, "index_%s.npz" % name), **rec)
+        print("index", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
+
+
+def gen_heads(importlib):
+    for name, (head, B, N, kind, wseed, fseed) in cases.HEAD_CASES.items():
+        mod = importlib.import_module(head)
+        model = cases.build_head(mod.get_model, wseed)
+        x = cases.cloud(kind, B, N, wseed + 7)            # [B,N,C]
+        xin = x.permute(0, 2, 1).contiguous()             # [B,C,N] model input
+        rec = {"input": xin.numpy(), "state_hash": np.array(cases.state_hash(model))}
+        acts = {}
+
+        def hook(tag):
+            def f(_m, _inp, out):
+                acts[tag] = (out[0].detach().contiguous().numpy(), out[1].detach().contiguous().numpy())
+            return f
+        for tag in ("sa1", "sa2", "sa3"):
+            if hasattr(model, tag):
+                getattr(model, tag).register_forward_hook(hook(tag))
+        args = [xin]
+        if head.startswith("translation"):
+            mean = torch.randn(B, 3, generator=torch.Generator().manual_seed(wseed + 9))
+            rec["mean"] = mean.numpy()
+            args.append(mean)
+        torch.manual_seed(fseed)
+        with torch.no_grad():
+            out = model(*args)
+        outs = out if isinstance(out, tuple) else (out,)
+        for i, o in enumerate(outs):
+            rec["out%d" % i] = o.detach().numpy()
+        for tag, (p, f) in acts.items():
+            rec[tag + "_points"] = p
+            rec[tag + "_feature"] = f
+        np.savez_compressed(os.path.join(HERE, "head_%s.npz" % name), **rec)
+        print("head", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
+
+
+def main():
+    torch.set_num_threads(8)
+    P, importlib = _ref()
+    gen_index(P)
+    gen_heads(importlib)
+    meta = {
+        "torch": torch.__version__,
+        "cpu_capability": torch.backends.cpu.get_cpu_capability(),
+        "threads": torch.get_num_threads(),
+        "config": torch.__config__.show().splitlines()[:12],
+        "generator": "tests/golden/make_goldens.py (reference imported read-only from %s)" % REF_MODEL,
+    }
+    with open(os.path.join(HERE, "meta.json"), "w") as fh:
+        json.dump(meta, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
