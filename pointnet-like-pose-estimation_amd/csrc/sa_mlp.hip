@@ -126,7 +126,7 @@ __device__ __forceinline__ void gemm_pass(floatx16 (&acc)[NTILE], const float *a
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
-    const int kcf = kWch / cw;  // multiple of 16 (cw <= 256)
+    const int kcf = (kWch / cw) & ~15;  // k-depth of a staged chunk: multiple of 16 (cw <= 256)
     const int nch = (L.cin_pad + kcf - 1) / kcf;
     const int CT = cw >> 5;
     Stage<NT> st;
@@ -316,6 +316,8 @@ __global__ __launch_bounds__(BM * 4) void sa_mlp_kernel(const MlpArgs A) {
 #define PN2_MLP_SIGS(X)                                                                    \
     X(1, 0, 0, 0) X(2, 0, 0, 0) X(3, 0, 0, 0) X(4, 0, 0, 0) X(4, 4, 0, 0) X(2, 4, 0, 0)   \
     X(1, 1, 1, 0) X(1, 1, 2, 0) X(1, 2, 2, 0) X(2, 2, 4, 0) X(1, 2, 4, 0) X(2, 2, 2, 0)
+// 32-row tiles (very wide inputs, e.g. a 512-channel layer) exist for single layers only
+#define PN2_MLP_SIGS32(X) X(1, 0, 0, 0) X(2, 0, 0, 0) X(3, 0, 0, 0) X(4, 0, 0, 0)
 
 // ------------------------------------------------------------------ BN/conv packing
 __global__ __launch_bounds__(256) void pack_layer_kernel(
@@ -398,7 +400,11 @@ static int make_plan(Plan &P, const pn2_sa_src &s, const pn2_mlp_layer *layers, 
     A.out = out;
     A.ostride = ostride;
     const int64_t coutL = layers[n - 1].cout;
-    P.BM = lds_bytes(128, A.ld, 0, 0) > 112 * 1024 ? 64 : 128;
+    // rows per workgroup: 128 when the activation tile leaves room for 2 workgroups' worth of
+    // other state, else 64, else 32 (single-layer launches only)
+    P.BM = 128;
+    if (lds_bytes(128, A.ld, 0, 0) > 112 * 1024) P.BM = 64;
+    if (lds_bytes(64, A.ld, 0, 0) > 144 * 1024) P.BM = 32;
     P.tiles = (M + P.BM - 1) / P.BM;
     // a single-layer launch can also split its columns over grid.y (nothing is recomputed)
     P.ysplit = 1;
@@ -421,6 +427,8 @@ static int make_plan(Plan &P, const pn2_sa_src &s, const pn2_mlp_layer *layers, 
     }
     if (P.lds > 160 * 1024)
         return set_error(PN2_EUNSUPPORTED, "pn2_sa_mlp_max_f32: LDS %zu > 160 KiB (ld=%d)", P.lds, A.ld);
+    if (P.BM == 32 && n > 1)
+        return set_error(PN2_EUNSUPPORTED, "pn2_sa_mlp_max_f32: 32-row tiles are single-layer only");
     return PN2_OK;
 }
 
@@ -451,13 +459,20 @@ static int try_launch(const Plan &P, hipStream_t st) {
             return set_error(PN2_EHIP, "pn2_sa_mlp_max_f32: memset: %s", hipGetErrorString(e));
     }
 #define PN2_TRY(t0, t1, t2, t3)                                                          \
-    if (P.T[0] == t0 && P.T[1] == t1 && P.T[2] == t2 && P.T[3] == t3) {                \
+    if (P.BM != 32 && P.T[0] == t0 && P.T[1] == t1 && P.T[2] == t2 && P.T[3] == t3) {  \
         const int rc = P.BM == 128 ? launch_sig<128, t0, t1, t2, t3>(P, st)              \
                                    : launch_sig<64, t0, t1, t2, t3>(P, st);              \
         return rc == PN2_OK ? 1 : rc;                                                    \
     }
     PN2_MLP_SIGS(PN2_TRY)
 #undef PN2_TRY
+#define PN2_TRY32(t0, t1, t2, t3)                                                        \
+    if (P.BM == 32 && P.T[0] == t0 && P.T[1] == t1 && P.T[2] == t2 && P.T[3] == t3) {  \
+        const int rc = launch_sig<32, t0, t1, t2, t3>(P, st);                            \
+        return rc == PN2_OK ? 1 : rc;                                                    \
+    }
+    PN2_MLP_SIGS32(PN2_TRY32)
+#undef PN2_TRY32
     return 0;
 }
 
@@ -501,30 +516,76 @@ static int validate(const pn2_sa_src *src, const pn2_mlp_layer *layers, int nlay
     return PN2_OK;
 }
 
-static bool fusable(const pn2_mlp_layer *layers, int nlayers) {
-    for (int l = 0; l < nlayers - 1; ++l)
-        if (layers[l].cout > kMaxSlice) return false;
-    return true;
+// A chain runs as consecutive fused segments; a segment ends after a layer wider than one
+// column slice (its output cannot stay in LDS) or at the end of the chain.  Segment outputs
+// go to two ping-pong [M][w] workspace buffers.  A segment with no compiled signature (or too
+// wide for LDS) runs layer by layer through the same workspace.
+static int seg_end(const pn2_mlp_layer *layers, int nlayers, int l0) {
+    int l = l0;
+    while (l < nlayers - 1 && layers[l].cout <= kMaxSlice) ++l;
+    return l;  // inclusive
+}
+
+static bool segment_fused(const pn2_sa_src &s, const pn2_mlp_layer *layers, int l0, int l1,
+                          int64_t M, int64_t K, int pool) {
+    Plan P;
+    if (make_plan(P, s, layers + l0, l1 - l0 + 1, pool, nullptr, layers[l1].cout, M, K) != PN2_OK)
+        return false;
+    bool found = false;
+#define PN2_HAS(t0, t1, t2, t3) \
+    if (P.BM != 32 && P.T[0] == t0 && P.T[1] == t1 && P.T[2] == t2 && P.T[3] == t3) found = true;
+    PN2_MLP_SIGS(PN2_HAS)
+#undef PN2_HAS
+#define PN2_HAS32(t0, t1, t2, t3) \
+    if (P.BM == 32 && P.T[0] == t0 && P.T[1] == t1 && P.T[2] == t2 && P.T[3] == t3) found = true;
+    PN2_MLP_SIGS32(PN2_HAS32)
+#undef PN2_HAS32
+    return found;
+}
+
+static pn2_sa_src rows_src(const float *rows, int64_t w, int64_t M, int64_t K) {
+    pn2_sa_src nx;
+    memset(&nx, 0, sizeof(nx));
+    nx.mode = PN2_SRC_ROWS;
+    nx.rows = rows;
+    nx.rs = w;
+    nx.B = 1; nx.S = M / K; nx.K = K;
+    return nx;
+}
+
+// workspace width needed: the widest layer output that has to round-trip through HBM
+static int64_t workspace_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers,
+                               int64_t M, int64_t K) {
+    int64_t w = 0;
+    for (int l0 = 0; l0 < nlayers;) {
+        const int l1 = seg_end(layers, nlayers, l0);
+        const bool last_seg = l1 == nlayers - 1;
+        pn2_sa_src src = l0 == 0 ? s : rows_src(nullptr, 0, M, K);
+        if (l0 > 0) src.rows = reinterpret_cast<const float *>(16);
+        if (!segment_fused(src, layers, l0, l1, M, K, last_seg ? 1 : 0))
+            for (int l = l0; l < l1; ++l) w = std::max(w, layers[l].cout);
+        if (!last_seg) w = std::max(w, layers[l1].cout);
+        l0 = l1 + 1;
+    }
+    return w;
 }
 
 extern "C" int64_t pn2_sa_mlp_workspace_bytes(const pn2_sa_src *src, const pn2_mlp_layer *layers,
                                               int nlayers) {
     int64_t M = 0, K = 1;
     if (validate(src, layers, nlayers, M, K) != PN2_OK) return -1;
-    if (fusable(layers, nlayers)) {
-        Plan P;
-        if (make_plan(P, *src, layers, nlayers, 1, nullptr, layers[nlayers - 1].cout, M, K) == PN2_OK) {
-            bool found = false;
-#define PN2_HAS(t0, t1, t2, t3) \
-    if (P.T[0] == t0 && P.T[1] == t1 && P.T[2] == t2 && P.T[3] == t3) found = true;
-            PN2_MLP_SIGS(PN2_HAS)
-#undef PN2_HAS
-            if (found) return 0;
-        }
-    }
-    int64_t w = 0;
-    for (int l = 0; l < nlayers - 1; ++l) w = std::max(w, layers[l].cout);
-    return 2 * M * w * 4;
+    return 2 * M * workspace_width(*src, layers, nlayers, M, K) * 4;
+}
+
+static int run_single(const pn2_sa_src &cur, const pn2_mlp_layer *layers, int l0, int l1,
+                      int pool, float *dst, int64_t ostride, int64_t M, int64_t K, hipStream_t st) {
+    Plan P;
+    int rc = make_plan(P, cur, layers + l0, l1 - l0 + 1, pool, dst, ostride, M, K);
+    if (rc != PN2_OK) return rc;
+    rc = try_launch(P, st);
+    if (rc < 0) return rc;
+    if (rc == 0) return set_error(PN2_EUNSUPPORTED, "pn2_sa_mlp_max_f32: no kernel for layers %d..%d", l0, l1);
+    return PN2_OK;
 }
 
 extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers,
@@ -538,40 +599,32 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
     if (M == 0) return PN2_OK;
     if (pool) PN2_REQUIRE(M % K == 0, "pn2_sa_mlp_max_f32: rows not a multiple of the group size");
     hipStream_t st = as_stream(stream);
-
-    if (fusable(layers, nlayers)) {
-        Plan P;
-        rc = make_plan(P, *src, layers, nlayers, pool, out, ostride, M, K);
-        if (rc == PN2_OK) {
-            rc = try_launch(P, st);
-            if (rc != 0) return rc < 0 ? rc : PN2_OK;
-        } else if (rc != PN2_EUNSUPPORTED) {
-            return rc;
-        }
-    }
-    // layer-by-layer through the workspace (two ping-pong [M][w] buffers)
-    int64_t w = 0;
-    for (int l = 0; l < nlayers - 1; ++l) w = std::max(w, layers[l].cout);
-    PN2_REQUIRE(workspace && workspace_bytes >= 2 * M * w * 4,
-                "pn2_sa_mlp_max_f32: this layer chain needs a %lld-byte workspace",
-                (long long)(2 * M * w * 4));
+    const int64_t w = workspace_width(*src, layers, nlayers, M, K);
+    if (w > 0)
+        PN2_REQUIRE(workspace && workspace_bytes >= 2 * M * w * 4,
+                    "pn2_sa_mlp_max_f32: this layer chain needs a %lld-byte workspace",
+                    (long long)(2 * M * w * 4));
     pn2_sa_src cur = *src;
-    for (int l = 0; l < nlayers; ++l) {
-        const bool last = l == nlayers - 1;
-        float *dst = last ? out : workspace + (l & 1) * M * w;
-        Plan P;
-        rc = make_plan(P, cur, layers + l, 1, last ? pool : 0, dst, last ? ostride : w, M, K);
-        if (rc != PN2_OK) return rc;
-        rc = try_launch(P, st);
-        if (rc < 0) return rc;
-        if (rc == 0) return set_error(PN2_EUNSUPPORTED, "pn2_sa_mlp_max_f32: no kernel for layer %d", l);
-        pn2_sa_src nx;
-        memset(&nx, 0, sizeof(nx));
-        nx.mode = PN2_SRC_ROWS;
-        nx.rows = dst;
-        nx.rs = w;
-        nx.B = 1; nx.S = M / K; nx.K = K;
-        cur = nx;
+    int buf = 0;
+    for (int l0 = 0; l0 < nlayers;) {
+        const int l1 = seg_end(layers, nlayers, l0);
+        const bool last_seg = l1 == nlayers - 1;
+        if (segment_fused(cur, layers, l0, l1, M, K, last_seg ? pool : 0)) {
+            float *dst = last_seg ? out : workspace + buf * M * w;
+            rc = run_single(cur, layers, l0, l1, last_seg ? pool : 0, dst, last_seg ? ostride : w,
+                            M, K, st);
+            if (rc != PN2_OK) return rc;
+            if (!last_seg) { cur = rows_src(dst, w, M, K); buf ^= 1; }
+        } else {
+            for (int l = l0; l <= l1; ++l) {
+                const bool last = l == nlayers - 1;
+                float *dst = last ? out : workspace + buf * M * w;
+                rc = run_single(cur, layers, l, l, last ? pool : 0, dst, last ? ostride : w, M, K, st);
+                if (rc != PN2_OK) return rc;
+                if (!last) { cur = rows_src(dst, w, M, K); buf ^= 1; }
+            }
+        }
+        l0 = l1 + 1;
     }
     return PN2_OK;
 }

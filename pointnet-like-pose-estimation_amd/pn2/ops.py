@@ -15,6 +15,7 @@ Ops (reference code each replaces, in /root/reference/model/pointnet2_utils.py):
   pn2::pack_layer     Conv2d 1x1 + BatchNorm2d (eval) parameters :150-156, :184-193
   pn2::sa_mlp_max_    gathered shared MLP + max :167-172, :211-218 (writes into `out`)
 """
+import contextlib
 from typing import List, Optional, Tuple
 
 import torch
@@ -24,6 +25,54 @@ from . import _lib
 from ._lib import MlpLayer, SaSrc, check, load
 
 _L = load()  # fail at import, loudly, if the native library is unavailable
+
+
+class KernelTimer:
+    """HIP-event timing of every libpn2 launch, recorded on the stream the launch is issued on
+    (torch's current stream), with each launch's algorithmic FLOPs / bytes."""
+
+    def __init__(self):
+        self.records = []  # (name, start_event, end_event, flops, bytes)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, e0, e1, flops, nbytes in self.records:
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["flops"] += flops
+            d["bytes"] += nbytes
+        return out
+
+
+_TIMER = None
+
+
+@contextlib.contextmanager
+def kernel_timer():
+    """Within this context every pn2 op launch is bracketed by HIP events."""
+    global _TIMER
+    prev, _TIMER = _TIMER, KernelTimer()
+    try:
+        yield _TIMER
+    finally:
+        _TIMER = prev
+
+
+def _run(name, fn, args, device, flops=0.0, nbytes=0.0):
+    t = _TIMER
+    if t is None:
+        check(fn(*args), name)
+        return
+    s = torch.cuda.current_stream(device)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    rc = fn(*args)
+    e1.record(s)
+    check(rc, name)
+    t.records.append((name, e0, e1, float(flops), float(nbytes)))
 
 
 def _dev(t: Tensor, what: str):
@@ -60,9 +109,10 @@ def fps(points: Tensor, npoint: int, start: Tensor) -> Tuple[Tensor, Tensor, Ten
     cpk = torch.empty(B, npoint, cp, dtype=torch.float32, device=points.device)
     ppk = torch.empty(B, N, cp, dtype=torch.float32, device=points.device)
     sb, sn, sc = points.stride()
-    check(_L.pn2_fps_f32(points.data_ptr(), B, N, C, sb, sn, sc, start.data_ptr(), npoint,
-                         idx.data_ptr(), newp.data_ptr(), cpk.data_ptr(), ppk.data_ptr(),
-                         _stream(points)), "pn2_fps_f32")
+    _run("pn2_fps_f32", _L.pn2_fps_f32,
+         (points.data_ptr(), B, N, C, sb, sn, sc, start.data_ptr(), npoint, idx.data_ptr(),
+          newp.data_ptr(), cpk.data_ptr(), ppk.data_ptr(), _stream(points)), points.device,
+         flops=float(B) * npoint * N * (3 * C + 2))
     return idx, newp, cpk, ppk
 
 
@@ -82,8 +132,8 @@ def pack_points(points: Tensor) -> Tensor:
     B, N, C = points.shape
     out = torch.empty(B, N, packed_stride(C), dtype=torch.float32, device=points.device)
     sb, sn, sc = points.stride()
-    check(_L.pn2_pack_points_f32(points.data_ptr(), B, N, C, sb, sn, sc, out.data_ptr(),
-                                 _stream(points)), "pn2_pack_points_f32")
+    _run("pn2_pack_points_f32", _L.pn2_pack_points_f32,
+         (points.data_ptr(), B, N, C, sb, sn, sc, out.data_ptr(), _stream(points)), points.device)
     return out
 
 
@@ -104,9 +154,11 @@ def ball_query(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, ns
         # the reference's `group_idx[mask] = group_first[mask]` fails the same way (:89)
         raise IndexError("query_ball_point: sample_number %d > number of points %d" % (nsample, N))
     out = torch.empty(B, S, nsample, dtype=torch.int64, device=pts_packed.device)
-    check(_L.pn2_ball_query_f32(pts_packed.data_ptr(), ctr_packed.data_ptr(), B, N, S, C,
-                                float(radius), nsample, out.data_ptr(), _stream(pts_packed)),
-          "pn2_ball_query_f32")
+    cp = pts_packed.shape[2]
+    _run("pn2_ball_query_f32", _L.pn2_ball_query_f32,
+         (pts_packed.data_ptr(), ctr_packed.data_ptr(), B, N, S, C, float(radius), nsample,
+          out.data_ptr(), _stream(pts_packed)), pts_packed.device,
+         nbytes=4.0 * cp * B * (N + S) + 8.0 * B * S * nsample)
     return out
 
 
@@ -122,8 +174,9 @@ def square_distance(src_packed: Tensor, dst_packed: Tensor, C: int) -> Tensor:
     B, S, _ = src_packed.shape
     N = dst_packed.shape[1]
     out = torch.empty(B, S, N, dtype=torch.float32, device=src_packed.device)
-    check(_L.pn2_square_distance_f32(src_packed.data_ptr(), dst_packed.data_ptr(), B, S, N, C,
-                                     out.data_ptr(), _stream(src_packed)), "pn2_square_distance_f32")
+    _run("pn2_square_distance_f32", _L.pn2_square_distance_f32,
+         (src_packed.data_ptr(), dst_packed.data_ptr(), B, S, N, C, out.data_ptr(),
+          _stream(src_packed)), src_packed.device)
     return out
 
 
@@ -142,8 +195,9 @@ def index_points(points: Tensor, idx: Tensor) -> Tensor:
     idx = idx.contiguous()
     out = torch.empty(B, M, C, dtype=torch.float32, device=points.device)
     sb, sn, sc = points.stride()
-    check(_L.pn2_index_points_f32(points.data_ptr(), B, N, C, sb, sn, sc, idx.data_ptr(), M,
-                                  out.data_ptr(), _stream(points)), "pn2_index_points_f32")
+    _run("pn2_index_points_f32", _L.pn2_index_points_f32,
+         (points.data_ptr(), B, N, C, sb, sn, sc, idx.data_ptr(), M, out.data_ptr(),
+          _stream(points)), points.device)
     return out
 
 
@@ -170,9 +224,9 @@ def group(points: Tensor, feature: Optional[Tensor], centers: Tensor, idx: Tenso
     else:
         fp = feature.data_ptr()
         fb, fn, fd = feature.stride()
-    check(_L.pn2_group_f32(points.data_ptr(), B, N, C, sb, sn, sc, fp, D, fb, fn, fd,
-                           centers.data_ptr(), S, idx.data_ptr(), K, int(feature_first),
-                           out.data_ptr(), _stream(points)), "pn2_group_f32")
+    _run("pn2_group_f32", _L.pn2_group_f32,
+         (points.data_ptr(), B, N, C, sb, sn, sc, fp, D, fb, fn, fd, centers.data_ptr(), S,
+          idx.data_ptr(), K, int(feature_first), out.data_ptr(), _stream(points)), points.device)
     return out
 
 
@@ -200,9 +254,9 @@ def pack_layer(weight: Tensor, bias: Optional[Tensor], gamma: Optional[Tensor],
     def p(t):
         return 0 if t is None else t.contiguous().data_ptr()
     keep = [None if t is None else t.contiguous() for t in (bias, gamma, beta, mean, var)]
-    check(_L.pn2_pack_layer_f32(w.data_ptr(), *[p(t) for t in keep], float(eps), cout, cin,
-                                wt.data_ptr(), al.data_ptr(), be.data_ptr(), _stream(weight)),
-          "pn2_pack_layer_f32")
+    _run("pn2_pack_layer_f32", _L.pn2_pack_layer_f32,
+         (w.data_ptr(), *[p(t) for t in keep], float(eps), cout, cin, wt.data_ptr(),
+          al.data_ptr(), be.data_ptr(), _stream(weight)), weight.device)
     return wt, al, be
 
 
@@ -267,9 +321,11 @@ def sa_mlp_max_(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor
     if ws_bytes < 0:
         check(-1, "pn2_sa_mlp_workspace_bytes")
     ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=points.device) if ws_bytes else None
-    check(_L.pn2_sa_mlp_max_f32(src, layers, n, 1, out.data_ptr(), out.stride(-2),
-                                0 if ws is None else ws.data_ptr(), ws_bytes, _stream(points)),
-          "pn2_sa_mlp_max_f32")
+    M = B * S * K
+    flops = 2.0 * M * sum(cins[i] * wts[i].shape[1] for i in range(n))
+    _run("pn2_sa_mlp_max_f32", _L.pn2_sa_mlp_max_f32,
+         (src, layers, n, 1, out.data_ptr(), out.stride(-2), 0 if ws is None else ws.data_ptr(),
+          ws_bytes, _stream(points)), points.device, flops=flops)
 
 
 @sa_mlp_max_.register_fake

@@ -57,6 +57,8 @@ def shard_range(global_batch, rank, world):
 def all_gather_rows(local, group=None):
     """Concatenate every rank's [b_r, ...] tensor along dim 0 (equal b_r; RCCL all_gather on
     GPU tensors, gloo on CPU ones)."""
+    if not dist.is_available() or not dist.is_initialized():
+        return local
     world = dist.get_world_size(group)
     if world == 1:
         return local

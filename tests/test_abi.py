@@ -1,0 +1,78 @@
+"""The C ABI library loads (no GPU needed) and exports every symbol include/pn2.h declares;
+argument validation happens before any device call, so the error paths run on CPU too."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "pn2.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pn2_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from pn2 import _lib
+    L = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) >= 13
+    for s in syms:
+        assert hasattr(L, s), s
+        assert s in _lib.SIGNATURES, "ctypes binding missing for " + s
+
+
+def test_abi_constants():
+    from pn2 import _lib
+    L = _lib.load()
+    assert L.pn2_abi_version() == _lib.ABI_VERSION
+    assert [L.pn2_packed_stride(c) for c in (3, 4, 10, 11, 16)] == [4, 8, 12, 12, 20]
+    assert [L.pn2_layer_cin_pad(c) for c in (3, 8, 131, 259, 323)] == [8, 8, 136, 264, 328]
+
+
+def test_validation_errors_without_gpu():
+    from pn2 import _lib
+    L = _lib.load()
+    rc = L.pn2_fps_f32(None, 1, 8, 3, 24, 3, 1, None, 4, None, None, None, None, None)
+    assert rc == -1 and b"null" in L.pn2_last_error()
+    rc = L.pn2_ball_query_f32(1, 1, 2, 8, 4, 3, 0.2, 9, 1, None)
+    assert rc == -1 and b"sample_number 9 > N 8" in L.pn2_last_error()
+    rc = L.pn2_fps_f32(1, 1, 8, 40, 320, 40, 1, 1, 4, 1, None, None, None, None)
+    assert rc == -2 and b"unsupported C" in L.pn2_last_error()
+
+
+def _layers(widths, cin):
+    from pn2 import _lib
+    arr = (_lib.MlpLayer * len(widths))()
+    for i, w in enumerate(widths):
+        arr[i].wt = arr[i].alpha = arr[i].beta = 16  # dummy non-null (never dereferenced)
+        arr[i].cin = cin if i == 0 else widths[i - 1]
+        arr[i].cout = w
+    return arr
+
+
+@pytest.mark.parametrize("widths,cin,mode,fused", [
+    ([64, 64, 128], 3, 0, True),        # SSG sa1
+    ([128, 128, 256], 131, 0, True),    # SSG sa2
+    ([32, 32, 64], 3, 1, True),         # MSG sa1 scale 0
+    ([64, 96, 128], 3, 1, True),        # MSG sa1 scale 2
+    ([128, 128, 256], 323, 1, True),    # MSG sa2 (feature-first, 320 + 3)
+    ([256, 512, 1024], 259, 2, False),  # group_all: hidden 512 > 256 -> layer by layer
+])
+def test_workspace_query(widths, cin, mode, fused):
+    from pn2 import _lib
+    L = _lib.load()
+    s = _lib.SaSrc()
+    s.mode = mode
+    s.pts = s.ctr = s.idx = s.feat = 16
+    s.B, s.N, s.C, s.S, s.K = 2, 1024, 3, 128, 32
+    s.D = cin - 3
+    if mode == 2:
+        s.S, s.K = 1, 1024
+    ws = L.pn2_sa_mlp_workspace_bytes(s, _layers(widths, cin), len(widths))
+    assert (ws == 0) == fused and ws >= 0

@@ -1,0 +1,167 @@
+"""GPU parity of the index-path ops through the C ABI (torch.ops.pn2.*) -- bit-exact against
+the reference's goldens and against the pinned CPU oracle on seeded random inputs."""
+import numpy as np
+import pytest
+import torch
+
+import cases
+import oracle
+from conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+INDEX = golden_names("index_")
+
+
+def _points(g):
+    return cases.as_layout(torch.from_numpy(g["points"]), str(g["layout"]))
+
+
+def _to_dev_view(p):
+    """Move a [B,N,C] view to the device keeping its storage layout (strided vs contig)."""
+    if p.stride(2) == 1:
+        return p.contiguous().to(DEV)
+    return p.permute(0, 2, 1).contiguous().to(DEV).permute(0, 2, 1)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _pn2():
+    import pn2  # noqa: F401
+    assert torch.cuda.is_available()
+
+
+@pytest.mark.parametrize("name", INDEX)
+def test_fps_matches_reference(name):
+    g = load_golden("index_%s.npz" % name)
+    pts = _to_dev_view(_points(g))
+    idx, newp, cpk, ppk = torch.ops.pn2.fps(pts, int(g["S"]), torch.from_numpy(g["start"]).to(DEV))
+    np.testing.assert_array_equal(idx.cpu().numpy(), g["fps_idx"])
+    np.testing.assert_array_equal(newp.cpu().numpy().view(np.uint32), g["new_points"].view(np.uint32))
+
+
+@pytest.mark.parametrize("name", INDEX)
+def test_ball_query_matches_reference(name):
+    import pn2
+    g = load_golden("index_%s.npz" % name)
+    pts = _to_dev_view(_points(g))
+    newp = torch.from_numpy(g["new_points"]).to(DEV)
+    i = 0
+    while "bq%d_K" % i in g:
+        r, K = float(g["bq%d_radius" % i]), int(g["bq%d_K" % i])
+        want = g["bq%d_idx" % i]
+        if want.size == 0:
+            with pytest.raises(IndexError):
+                pn2.query_ball_point(r, K, pts, newp)
+        else:
+            got = pn2.query_ball_point(r, K, pts, newp)
+            assert got.dtype == torch.int64
+            np.testing.assert_array_equal(got.cpu().numpy(), want)
+        i += 1
+
+
+@pytest.mark.parametrize("name", INDEX)
+def test_fused_fps_packing_feeds_ball_query(name):
+    """The packed records emitted by the FPS kernel give the same ball query as packing the
+    tensors separately (the SA module's path)."""
+    g = load_golden("index_%s.npz" % name)
+    pts = _to_dev_view(_points(g))
+    N, C = pts.shape[1], pts.shape[2]
+    idx, newp, cpk, ppk = torch.ops.pn2.fps(pts, int(g["S"]), torch.from_numpy(g["start"]).to(DEV))
+    r, K = float(g["bq0_radius"]), int(g["bq0_K"])
+    if K > N:
+        pytest.skip("K > N")
+    got = torch.ops.pn2.ball_query(ppk, cpk, C, r, K)
+    np.testing.assert_array_equal(got.cpu().numpy(), g["bq0_idx"])
+
+
+@pytest.mark.parametrize("name", [n for n in INDEX if "sqdist" in load_golden("index_%s.npz" % n)])
+def test_square_distance_bit_exact(name):
+    import pn2
+    g = load_golden("index_%s.npz" % name)
+    got = pn2.square_distance(torch.from_numpy(g["new_points"]).to(DEV), _to_dev_view(_points(g)))
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), g["sqdist"].view(np.uint32))
+
+
+@pytest.mark.parametrize("C,layout", [(3, "strided"), (3, "contig"), (6, "contig"), (10, "strided"),
+                                      (13, "contig"), (16, "strided")])
+@pytest.mark.parametrize("N", [1, 2, 63, 65, 300, 1000, 2049, 4096])
+def test_fps_and_ball_query_random_vs_oracle(C, layout, N):
+    import pn2
+    gen = torch.Generator().manual_seed(1000 * C + N)
+    B = 3
+    p = torch.randn(B, N, C, generator=gen) * 0.5
+    p = cases.as_layout(p, layout)
+    S = min(N, 300) if N > 4 else 6   # S may exceed N in the reference; covered by goldens too
+    start = torch.randint(0, N, (B,), generator=gen)
+    want = oracle.farthest_point_sample(p, S, start)
+    dp = _to_dev_view(p)
+    idx, newp, cpk, ppk = torch.ops.pn2.fps(dp, S, start.to(DEV))
+    np.testing.assert_array_equal(idx.cpu().numpy(), want)
+    newp_h = oracle.index_points(p, want)
+    for r, K in ((0.3, min(N, 16)), (0.8, min(N, 64))):
+        exp = oracle.query_ball_point(r, K, p, newp_h)
+        got = torch.ops.pn2.ball_query(ppk, cpk, C, r, K)
+        np.testing.assert_array_equal(got.cpu().numpy(), exp)
+        got2 = pn2.query_ball_point(r, K, dp, newp)
+        np.testing.assert_array_equal(got2.cpu().numpy(), exp)
+
+
+def test_index_points_and_group_exact():
+    import pn2
+    gen = torch.Generator().manual_seed(5)
+    B, N, C, D, S, K = 2, 200, 3, 7, 16, 8
+    pts = torch.randn(B, C, N, generator=gen).permute(0, 2, 1)
+    feat = torch.randn(B, D, N, generator=gen).permute(0, 2, 1)
+    ctr = torch.randn(B, S, C, generator=gen)
+    idx = torch.randint(0, N, (B, S, K), generator=gen)
+    dp, dfe = _to_dev_view(pts), _to_dev_view(feat)
+    got = pn2.index_points(dp, idx.to(DEV))
+    np.testing.assert_array_equal(got.cpu().numpy(), oracle.index_points(pts, idx))
+    for ff in (False, True):
+        got = torch.ops.pn2.group(dp, dfe, ctr.to(DEV), idx.to(DEV), ff)
+        np.testing.assert_array_equal(got.cpu().numpy(), oracle.group(pts, feat, idx, ctr, feature_first=ff))
+    got = torch.ops.pn2.group(dp, None, ctr.to(DEV), idx.to(DEV), False)
+    np.testing.assert_array_equal(got.cpu().numpy(), oracle.group(pts, None, idx, ctr))
+
+
+def test_sample_and_group_matches_oracle():
+    import pn2
+    gen = torch.Generator().manual_seed(9)
+    B, N, D = 2, 512, 5
+    pts = cases.cloud("uniform3", B, N, 9)
+    feat = torch.randn(B, N, D, generator=gen)
+    torch.manual_seed(77)
+    newp, newf, grouped, fps_idx = pn2.sample_and_group(pts.to(DEV), feat.to(DEV), 64, 16, 0.3, returnfps=True)
+    torch.manual_seed(77)
+    start = torch.randint(0, N, (B,), dtype=torch.long)
+    f = oracle.farthest_point_sample(pts, 64, start)
+    np.testing.assert_array_equal(fps_idx.cpu().numpy(), f)
+    c = oracle.index_points(pts, f)
+    idx = oracle.query_ball_point(0.3, 16, pts, c)
+    np.testing.assert_array_equal(newf.cpu().numpy(), oracle.group(pts, feat, idx, c))
+    np.testing.assert_array_equal(grouped.cpu().numpy(), oracle.index_points(feat, idx))
+    np2, nf2 = pn2.sample_and_group_all(pts.to(DEV), feat.to(DEV))
+    assert np2.shape == (B, 1, 3) and float(np2.abs().sum()) == 0.0
+    np.testing.assert_array_equal(nf2.cpu().numpy()[:, 0], np.concatenate([pts.numpy(), feat.numpy()], -1))
+
+
+def test_errors_are_loud():
+    import pn2
+    from pn2._lib import Pn2Error
+    pts = torch.rand(1, 8, 3, device=DEV)
+    with pytest.raises(IndexError):
+        pn2.query_ball_point(0.2, 9, pts, pts[:, :2])
+    with pytest.raises(RuntimeError):
+        pn2.farthest_point_sample(torch.rand(1, 8, 3), 4)  # CPU tensor: no CPU path
+    with pytest.raises(Pn2Error):
+        torch.ops.pn2.fps(torch.rand(1, 8, 40, device=DEV), 4, torch.zeros(1, dtype=torch.long, device=DEV))
+
+
+def test_fps_stress_size_vs_oracle():
+    """STRESS config geometry (N=16384) for two clouds, plus a 2048-point one-hot pose cloud."""
+    for kind, B, N, S in (("uniform3", 2, 16384, 512), ("onehot10", 2, 2048, 512)):
+        p = cases.as_layout(cases.cloud(kind, B, N, 3), "strided")
+        start = torch.tensor([5, N - 1])
+        want = oracle.farthest_point_sample(p, S, start)
+        idx = torch.ops.pn2.fps(_to_dev_view(p), S, start.to(DEV))[0]
+        np.testing.assert_array_equal(idx.cpu().numpy(), want)

@@ -1,0 +1,189 @@
+"""GPU parity of the SA modules and full heads (fused path) against the reference's goldens,
+plus full-size BASELINE configs checked through size-independent properties.
+
+Tolerance for float features (north star: 1e-5 relative): |got - ref| <= 1e-5 * |ref| +
+1e-5 * max|ref| -- the absolute floor covers near-zero ReLU outputs whose relative error is
+meaningless; indices and centroid coordinates are compared bit-for-bit."""
+import numpy as np
+import pytest
+import torch
+
+import cases
+import oracle
+from conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+RTOL = 1e-5
+
+
+def assert_feat_close(got, want, rtol=RTOL):
+    got = np.asarray(got, np.float64)
+    want = np.asarray(want, np.float64)
+    atol = rtol * max(float(np.abs(want).max()), 1e-30)
+    np.testing.assert_allclose(got, want, rtol=rtol, atol=atol)
+
+
+def _head(name):
+    from pn2 import heads as H
+    head, B, N, kind, wseed, fseed = cases.HEAD_CASES[name]
+    model = cases.build_head(H.HEADS[head], wseed)
+    return model, head, fseed
+
+
+@pytest.mark.parametrize("name", golden_names("head_"))
+def test_head_matches_reference(name):
+    g = load_golden("head_%s.npz" % name)
+    model, head, fseed = _head(name)
+    assert cases.state_hash(model) == str(g["state_hash"])
+    model = model.to(DEV).eval()
+    acts = {}
+    for tag in ("sa1", "sa2", "sa3"):
+        if hasattr(model, tag):
+            getattr(model, tag).register_forward_hook(
+                lambda m, i, o, tag=tag: acts.__setitem__(tag, (o[0].cpu().numpy(), o[1].cpu().numpy())))
+    args = [torch.from_numpy(g["input"]).to(DEV)]
+    if "mean" in g:
+        args.append(torch.from_numpy(g["mean"]).to(DEV))
+    torch.manual_seed(fseed)
+    with torch.no_grad():
+        out = model(*args)
+    for tag, (p, f) in acts.items():
+        np.testing.assert_array_equal(p.view(np.uint32), g[tag + "_points"].view(np.uint32),
+                                      err_msg=tag + " centroids")
+        assert_feat_close(f, g[tag + "_feature"])
+    outs = out if isinstance(out, tuple) else (out,)
+    for i, o in enumerate(outs):
+        if o.dtype == torch.int64:
+            np.testing.assert_array_equal(o.cpu().numpy(), g["out%d" % i])
+        else:
+            assert_feat_close(o.cpu().numpy(), g["out%d" % i], rtol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["cls_ssg", "cls_msg"])
+def test_reference_input_layout_transposed(name):
+    """The training loop feeds points.transpose(2,1) of a contiguous [B,N,C] tensor
+    (train_rotation.py:116); the drop-in must accept that view and give the same numbers."""
+    g = load_golden("head_%s.npz" % name)
+    model, head, fseed = _head(name)
+    model = model.to(DEV).eval()
+    x = torch.from_numpy(g["input"])
+    xt = x.permute(0, 2, 1).contiguous().to(DEV).permute(0, 2, 1)
+    torch.manual_seed(fseed)
+    with torch.no_grad():
+        a = model(x.to(DEV))
+    torch.manual_seed(fseed)
+    with torch.no_grad():
+        b = model(xt)
+    # C=3: both layouts sum the 3 channels in the same order -> identical results
+    np.testing.assert_array_equal(a[1].cpu().numpy(), b[1].cpu().numpy())
+
+
+def _torch_sa_reference(sa, pts_bnc, feat_bnd, start):
+    """fp32 torch-GPU evaluation of the reference formulation of one SSG layer (MIOpen conv +
+    BN), with the oracle's indices -- the float reference for the fused MLP kernel."""
+    from pn2.pointnet2_utils import _torch_group, _torch_mlp_max
+    B, N, C = pts_bnc.shape
+    f = oracle.farthest_point_sample(pts_bnc.cpu(), sa.point_number, start)
+    newp = oracle.index_points(pts_bnc.cpu(), f)
+    idx = oracle.query_ball_point(sa.radius, sa.sample_number, pts_bnc.cpu(), newp)
+    with torch.no_grad():
+        g = _torch_group(pts_bnc, torch.from_numpy(idx).to(DEV), torch.from_numpy(newp).to(DEV),
+                         feat_bnd, False)
+        return newp, _torch_mlp_max(g, sa.mlp_convs, sa.mlp_bns)
+
+
+def test_ssg_baseline_config_full_size():
+    """BASELINE config 2 (pointnet2_cls_ssg, B=32, N=1024): sa1 indices exact vs oracle for the
+    whole batch, features vs the fp32 torch formulation."""
+    from pn2 import heads as H
+    torch.manual_seed(0)
+    model = H.ClsSSG().eval()
+    cases.randomize_bn(model, 1)
+    model = model.to(DEV)
+    B, N = 32, 1024
+    x = cases.cloud("uniform3", B, N, 42).permute(0, 2, 1).contiguous()
+    torch.manual_seed(5)
+    with torch.no_grad():
+        newp, feat = model.sa1(x.to(DEV), None)
+    torch.manual_seed(5)
+    start = torch.randint(0, N, (B,), dtype=torch.long)
+    want_p, want_f = _torch_sa_reference(model.sa1, x.to(DEV).permute(0, 2, 1), None, start)
+    np.testing.assert_array_equal(newp.permute(0, 2, 1).cpu().numpy(), want_p)
+    assert_feat_close(feat.cpu().numpy(), want_f.cpu().numpy())
+    # the whole forward runs and is deterministic
+    torch.manual_seed(7)
+    with torch.no_grad():
+        o1 = model(x.to(DEV))
+    torch.manual_seed(7)
+    with torch.no_grad():
+        o2 = model(x.to(DEV))
+    np.testing.assert_array_equal(o1[0].cpu().numpy(), o2[0].cpu().numpy())
+
+
+def test_msg_baseline_config_full_size():
+    """BASELINE config 3 (pointnet2_cls_msg, B=32, N=4096): shapes, determinism, and the
+    autograd (torch) path agreeing with the fused path within tolerance."""
+    from pn2 import heads as H
+    torch.manual_seed(1)
+    model = H.ClsMSG().eval()
+    cases.randomize_bn(model, 2)
+    model = model.to(DEV)
+    B, N = 32, 4096
+    x = cases.cloud("uniform3", B, N, 43).permute(0, 2, 1).contiguous().to(DEV)
+    torch.manual_seed(3)
+    with torch.no_grad():
+        p1, f1 = model.sa1(x, None)
+    torch.manual_seed(3)
+    p2, f2 = model.sa1._forward_autograd(x, None)
+    np.testing.assert_array_equal(p1.cpu().numpy(), p2.detach().cpu().numpy())
+    assert f1.shape == (B, 320, 512)
+    assert_feat_close(f1.cpu().numpy(), f2.detach().cpu().numpy())
+
+
+def test_pose_heads_sharded_equals_unsharded():
+    """BASELINE config 4 semantics on one GPU: rotation_ssg + translation_ssg B=64 N=2048
+    one-hot; running the batch as 8 shards (with the full-batch FPS draws sliced) reproduces
+    the unsharded result bit-for-bit."""
+    from pn2 import heads as H
+    from pn2 import shard
+    torch.manual_seed(2)
+    rot = H.RotationSSG().eval()
+    cases.randomize_bn(rot, 3)
+    rot = rot.to(DEV)
+    B, N, W = 64, 2048, 8
+    x = cases.cloud("onehot10", B, N, 44).permute(0, 2, 1).contiguous().to(DEV)
+    torch.manual_seed(11)
+    with torch.no_grad():
+        full = rot(x)
+    parts = []
+    for r in range(W):
+        lo, hi = shard.shard_range(B, r, W)
+        torch.manual_seed(11)
+        with torch.no_grad(), shard.batch_shard(B, lo):
+            parts.append(rot(x[lo:hi]))
+    got = torch.cat(parts)
+    np.testing.assert_array_equal(got.cpu().numpy(), full.cpu().numpy())
+
+
+def test_stress_config_geometry():
+    """BASELINE config 5 geometry (B=128, N=16384): the FPS/ball-query front end of sa1 on 2
+    clouds of the batch vs the oracle (indices bit-exact)."""
+    import pn2
+    B, N, S, K = 128, 16384, 512, 32
+    x = cases.cloud("uniform3", B, N, 45)
+    xs = cases.as_layout(x, "strided")
+    start = torch.randint(0, N, (B,), generator=torch.Generator().manual_seed(0))
+    d = xs.permute(0, 2, 1).contiguous().to(DEV).permute(0, 2, 1)
+    idx, newp, cpk, ppk = torch.ops.pn2.fps(d, S, start.to(DEV))
+    bq = torch.ops.pn2.ball_query(ppk, cpk, 3, 0.2, K)
+    for b in (0, 97):
+        f = oracle.farthest_point_sample(xs[b:b + 1], S, start[b:b + 1])
+        np.testing.assert_array_equal(idx[b:b + 1].cpu().numpy(), f)
+        c = oracle.index_points(xs[b:b + 1], f)
+        np.testing.assert_array_equal(bq[b:b + 1].cpu().numpy(), oracle.query_ball_point(0.2, K, xs[b:b + 1], c))
+    # sortedness/padding property over the whole batch
+    q = bq.cpu().numpy()
+    first = q[:, :, :1]
+    d_ = np.diff(q, axis=-1)
+    assert ((d_ > 0) | ((d_ <= 0) & (q[:, :, 1:] == first))).all()
