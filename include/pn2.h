@@ -93,13 +93,18 @@ int pn2_group_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,
                   const float *ctr, int64_t S, const int64_t *idx, int64_t K, int feature_first,
                   float *out, void *stream);
 
-/* One shared-MLP layer packed for the kernel: wt [cin_pad][cout] (= W^T, zero rows past cin),
- * alpha[cout], beta[cout] such that layer(x) = relu(alpha * (W x) + beta), i.e. the eval-mode
- * BatchNorm2d folded with the conv bias.  cin_pad = pn2_layer_cin_pad(cin). */
+/* One shared-MLP layer packed for the kernels: wt = W^T pair-interleaved, [cin_pad/2][cout][2]
+ * (element (k, o) at ((k>>1)*cout + o)*2 + (k&1), zero rows past cin), alpha[cout], beta[cout]
+ * such that layer(x) = relu(alpha * (W x) + beta): the eval-mode BatchNorm2d folded with the
+ * conv bias.  The kernels lay a row out as [features | xyz]; `rot` is the number of leading
+ * input channels of W that are xyz (C for sample_and_group / group_all first layers, whose
+ * reference order is [xyz, features]; 0 otherwise): row k of wt is input channel (k+rot)%cin.
+ * cin_pad = pn2_layer_cin_pad(cin). */
 int64_t pn2_layer_cin_pad(int64_t cin);
 int pn2_pack_layer_f32(const float *W, const float *bias, const float *gamma, const float *beta,
                        const float *mean, const float *var, double eps, int64_t cout,
-                       int64_t cin, float *wt, float *alpha, float *beta_out, void *stream);
+                       int64_t cin, int64_t rot, float *wt, float *alpha, float *beta_out,
+                       void *stream);
 
 /* Source of the MLP's input rows. */
 #define PN2_SRC_GROUP_XYZ_FIRST 0  /* sample_and_group:  [xyz-ctr, feat] rows of group idx   */

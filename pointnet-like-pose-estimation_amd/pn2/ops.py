@@ -240,14 +240,15 @@ def _(points, feature, centers, idx, feature_first):
 @torch.library.custom_op("pn2::pack_layer", mutates_args=())
 def pack_layer(weight: Tensor, bias: Optional[Tensor], gamma: Optional[Tensor],
                beta: Optional[Tensor], mean: Optional[Tensor], var: Optional[Tensor],
-               eps: float) -> Tuple[Tensor, Tensor, Tensor]:
-    """Conv2d 1x1 weight [cout,cin,1,1] (+ bias) and eval BatchNorm2d stats -> (W^T padded
-    [cin_pad,cout], alpha [cout], beta [cout]) with layer(x) = relu(alpha*(W x) + beta)."""
+               eps: float, rot: int) -> Tuple[Tensor, Tensor, Tensor]:
+    """Conv2d 1x1 weight [cout,cin,1,1] (+ bias) and eval BatchNorm2d stats -> (W^T pair-packed
+    [cin_pad/2,cout,2], alpha [cout], beta [cout]) with layer(x) = relu(alpha*(W x) + beta).
+    rot: leading xyz input channels moved behind the features (the kernels' row order)."""
     _dev(weight, "pn2::pack_layer")
     cout, cin = weight.shape[0], weight.shape[1]
     w = weight.reshape(cout, cin).contiguous()
     dev = weight.device
-    wt = torch.empty(cin_pad(cin), cout, dtype=torch.float32, device=dev)
+    wt = torch.empty(cin_pad(cin) // 2, cout, 2, dtype=torch.float32, device=dev)
     al = torch.empty(cout, dtype=torch.float32, device=dev)
     be = torch.empty(cout, dtype=torch.float32, device=dev)
 
@@ -255,16 +256,16 @@ def pack_layer(weight: Tensor, bias: Optional[Tensor], gamma: Optional[Tensor],
         return 0 if t is None else t.contiguous().data_ptr()
     keep = [None if t is None else t.contiguous() for t in (bias, gamma, beta, mean, var)]
     _run("pn2_pack_layer_f32", _L.pn2_pack_layer_f32,
-         (w.data_ptr(), *[p(t) for t in keep], float(eps), cout, cin, wt.data_ptr(),
+         (w.data_ptr(), *[p(t) for t in keep], float(eps), cout, cin, int(rot), wt.data_ptr(),
           al.data_ptr(), be.data_ptr(), _stream(weight)), weight.device)
     return wt, al, be
 
 
 @pack_layer.register_fake
-def _(weight, bias, gamma, beta, mean, var, eps):
+def _(weight, bias, gamma, beta, mean, var, eps, rot):
     cout, cin = weight.shape[0], weight.shape[1]
     e = weight.new_empty
-    return e(cin_pad(cin), cout), e(cout), e(cout)
+    return e(cin_pad(cin) // 2, cout, 2), e(cout), e(cout)
 
 
 # ------------------------------------------------------------------------------ sa_mlp_max_
@@ -314,7 +315,7 @@ def sa_mlp_max_(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor
         layers[i].alpha = alphas[i].data_ptr()
         layers[i].beta = betas[i].data_ptr()
         layers[i].cin = cins[i]
-        layers[i].cout = wts[i].shape[1]
+        layers[i].cout = wts[i].shape[1]  # [cin_pad/2, cout, 2]
     if out.stride(-1) != 1:
         raise ValueError("pn2::sa_mlp_max_: out must have unit column stride")
     ws_bytes = int(_L.pn2_sa_mlp_workspace_bytes(src, layers, n))
@@ -322,7 +323,7 @@ def sa_mlp_max_(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor
         check(-1, "pn2_sa_mlp_workspace_bytes")
     ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=points.device) if ws_bytes else None
     M = B * S * K
-    flops = 2.0 * M * sum(cins[i] * wts[i].shape[1] for i in range(n))
+    flops = 2.0 * M * sum(cins[i] * wts[i].shape[1] for i in range(n))  # algorithmic, cin unpadded
     _run("pn2_sa_mlp_max_f32", _L.pn2_sa_mlp_max_f32,
          (src, layers, n, 1, out.data_ptr(), out.stride(-2), 0 if ws is None else ws.data_ptr(),
           ws_bytes, _stream(points)), points.device, flops=flops)

@@ -50,19 +50,21 @@ def _needs_autograd(module, *tensors):
         t is not None and t.requires_grad for t in tensors)
 
 
-def _pack_chain(convs, bns, cache):
+def _pack_chain(convs, bns, cache, rot0):
     """Fold each Conv2d-1x1 + eval BatchNorm2d into (W^T, alpha, beta); cached until any
-    parameter/buffer changes (data_ptr or in-place version)."""
+    parameter/buffer changes (data_ptr or in-place version).  rot0: xyz channels leading the
+    first layer's input in the reference's order (the kernels put them behind the features)."""
     tensors = []
     for conv, bn in zip(convs, bns):
         tensors += [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
-    key = tuple((None if t is None else (t.data_ptr(), t._version)) for t in tensors)
+    key = (rot0,) + tuple((None if t is None else (t.data_ptr(), t._version)) for t in tensors)
     if cache.get("key") != key:
         wts, als, bes, cins = [], [], [], []
         with torch.no_grad():
-            for conv, bn in zip(convs, bns):
+            for li, (conv, bn) in enumerate(zip(convs, bns)):
                 wt, al, be = ops.pack_layer(conv.weight, conv.bias, bn.weight, bn.bias,
-                                            bn.running_mean, bn.running_var, float(bn.eps))
+                                            bn.running_mean, bn.running_var, float(bn.eps),
+                                            rot0 if li == 0 else 0)
                 wts.append(wt)
                 als.append(al)
                 bes.append(be)
@@ -166,7 +168,9 @@ class PointNetSetAbstraction(nn.Module):
         pts = points.permute(0, 2, 1)
         feat = None if feature is None else _channels_last(feature)
         B, N, C = pts.shape
-        wts, als, bes, cins = _pack_chain(self.mlp_convs, self.mlp_bns, self._pack_cache)
+        # reference row order is [xyz, feature] (:114, :139); kernels use [feature, xyz]
+        rot0 = C if feat is not None else 0
+        wts, als, bes, cins = _pack_chain(self.mlp_convs, self.mlp_bns, self._pack_cache, rot0)
         cout = wts[-1].shape[1]
         dev = pts.device
         if self.group_all:
@@ -227,7 +231,8 @@ class PointNetSetAbstractionMsg(nn.Module):
         B, N, C = pts.shape
         S = self.point_number
         dev = pts.device
-        chains = [_pack_chain(self.conv_blocks[i], self.bn_blocks[i], self._pack_cache[i])
+        # MSG row order is already [feature, xyz] (:209): no rotation
+        chains = [_pack_chain(self.conv_blocks[i], self.bn_blocks[i], self._pack_cache[i], 0)
                   for i in range(len(self.radius_list))]
         total = sum(ch[0][-1].shape[1] for ch in chains)
         _, new_points, cpk, ppk = ops.fps(pts, S, _draw_start(B, N, dev))
