@@ -3,26 +3,42 @@
 // Replaces farthest_point_sample (/root/reference/model/pointnet2_utils.py:47-68) and the
 // index_points(points, fps_idx) that follows it (pointnet2_utils.py:106, 201).
 //
-// One workgroup per cloud.  The cloud lives in registers for the whole run (PPT points per
-// lane, point n = j*NT + lane-in-block so the loads coalesce for the reference's [B,C,N]
-// input), the running min-distance too (as the uint bits of a non-negative float, so every
-// compare/max is an integer op).  One iteration =
-//   distance of every point to the current centroid in the reference's exact float32 order
-//   (differences, exact squares, layout-dependent channel sum, no FMA contraction) ->
-//   strict-< min update -> per-lane argmax -> wave argmax by DPP (max value, then min index:
-//   torch.max returns the FIRST maximum) -> [NW > 1] one LDS slot per wave + ONE barrier
-//   (slots double-buffered by iteration parity) -> every wave re-reduces the NW slots itself,
-//   so the new centroid's coordinates arrive by v_readlane / LDS broadcast with no second
-//   barrier.
+// One workgroup per cloud.  Lane t of the block owns the CONTIGUOUS points t*PPT .. t*PPT+PPT-1
+// and keeps them in registers for the whole run, together with their running min-distance (the
+// uint bits of a non-negative float, so compares/maxima are integer ops).  Because ownership is
+// contiguous and in lane/wave order, "the first index among the maxima" (torch.max's tie rule)
+// is simply the first lane -- then the first wave -- that holds the maximum: one DPP max per
+// level plus a ballot, no second (index) reduction.  One iteration:
+//   branchless distance of every owned point to the centroid in the reference's exact float32
+//   order (differences, exact squares, layout-dependent channel sum, no FMA contraction) ->
+//   strict-< min update -> per-lane first-argmax (v_cndmask, no exec branches) -> wave max by DPP
+//   + ballot/ctz for the owner lane -> [NW > 1] the owner writes {max, index, coordinates} to its
+//   wave's LDS slot (double-buffered by iteration parity), ONE barrier, every wave reads all NW
+//   slots (one lane each), DPP max over a 16-lane row + ballot picks the winning wave and
+//   v_readlane broadcasts its index/coordinates.  No second barrier, no global memory in the loop.
 // The sampled indices are kept in LDS and written, with the gathered centroids and the packed
 // (coords, ssq) records the ball query reads, after the serial loop.
 #include "pn2_internal.h"
 
+#include <stdlib.h>
+
 namespace pn2 {
 
 constexpr int kFpsMaxS = 8192;
+constexpr int kFpsLdsCloud = 128 * 1024;  // bytes of LDS a cloud copy may take
 
-template <int NT, int PPT, int CM, bool FIXED>
+// max over the first 16 lanes (row 0), result valid in every lane of row 0
+__device__ __forceinline__ unsigned row_max_u32(unsigned v) {
+    v = max(v, PN2_DPP(v, 0xB1));
+    v = max(v, PN2_DPP(v, 0x4E));
+    v = max(v, PN2_DPP(v, 0x141));
+    v = max(v, PN2_DPP(v, 0x140));
+    return v;
+}
+
+// LDSC: keep a copy of the cloud in LDS (N*CM floats) so the winner's coordinates are one
+// broadcast ds_read; otherwise they travel with the per-wave slots.
+template <int NT, int PPT, int CM, bool FIXED, bool LDSC>
 __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, int N, int Crt,
                                                  int64_t sb, int64_t sn, int64_t sc, int kind,
                                                  const int64_t *__restrict__ start, int S,
@@ -31,7 +47,8 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
                                                  float *__restrict__ out_packed,
                                                  float *__restrict__ pts_packed, int cp) {
     constexpr int NW = NT / 64;
-    constexpr int SLOT = CM + 2;
+    static_assert(NW <= 16, "one 16-lane row reduces the wave slots");
+    constexpr int SLOT = (CM + 2 + 3) & ~3;  // {max, index, coords...} padded to 16 bytes
     const int C = FIXED ? CM : Crt;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -39,99 +56,150 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
     const int b = blockIdx.x;
     const float *P = pts + (int64_t)b * sb;
 
-    __shared__ int sidx[kFpsMaxS];
-    __shared__ float slots[2][NW][SLOT];
+    extern __shared__ __attribute__((aligned(16))) float fsm[];
+    int *sidx = reinterpret_cast<int *>(fsm);                          // [S]
+    unsigned long long *key = reinterpret_cast<unsigned long long *>(  // [3] (LDSC)
+        fsm + ((S + 3) & ~3));
+    float *slots = fsm + ((S + 3) & ~3) + 8;                            // [2][NW][SLOT] (!LDSC)
+    constexpr int CS = CM == 3 ? 4 : CM;  // cloud row stride (16-byte rows for xyz)
+    float *cloud = slots + (LDSC ? 0 : 2 * NW * SLOT);                  // [N][CS] (LDSC)
 
-    // ---- load the cloud into registers (and emit the packed copy for the ball query)
-    float p[PPT][CM];
+    // ---- load the owned points into registers (and emit the packed copy for the ball query).
+    // Points are held in pairs (one packed v_pk_* op computes two distances).  Lanes past the
+    // end own padding points: coordinates 0, distance 0 -- they never beat a real point (real
+    // points precede them and ties go to the first index).
+    constexpr int PH = (PPT + 1) / 2;
+    pn2_f2 q[PH][CM];
     unsigned dist[PPT];
+    int rule[PH];  // a pair shares its rule: the strided tail starts at an even index
 #pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int n = j * NT + tid;
-        const bool valid = n < N;
+    for (int j = 0; j < 2 * PH; ++j) {
+        const int n = tid * PPT + j;
+        const bool valid = j < PPT && n < N;
+        float pj[CM];
 #pragma unroll
-        for (int k = 0; k < CM; ++k)
-            p[j][k] = (valid && k < C) ? P[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
-        dist[j] = valid ? __float_as_uint(1e10f) : 0u;
-        if (valid && pts_packed) {
-            float sq[CM];
+        for (int k = 0; k < CM; ++k) {
+            pj[k] = (valid && k < C) ? P[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
+            q[j >> 1][k][j & 1] = pj[k];
+        }
+        if (j < PPT) dist[j] = valid ? __float_as_uint(1e10f) : 0u;
+        if ((j & 1) == 0) rule[j >> 1] = point_rule(kind, n, N);
+        if (valid) {
+            if constexpr (LDSC) {
 #pragma unroll
-            for (int k = 0; k < CM; ++k) sq[k] = __fmul_rn(p[j][k], p[j][k]);
-            float *dst = pts_packed + ((int64_t)b * N + n) * cp;
+                for (int k = 0; k < CS; ++k) cloud[n * CS + k] = k < CM ? pj[k] : 0.f;
+            }
+            if (pts_packed) {
+                float sq[CM];
 #pragma unroll
-            for (int k = 0; k < CM; ++k)
-                if (k < C) dst[k] = p[j][k];
-            dst[C] = layout_sum<CM>(sq, C, point_rule(kind, n, N));
-            for (int k = C + 1; k < cp; ++k) dst[k] = 0.f;
+                for (int k = 0; k < CM; ++k) sq[k] = __fmul_rn(pj[k], pj[k]);
+                float *dst = pts_packed + ((int64_t)b * N + n) * cp;
+#pragma unroll
+                for (int k = 0; k < CM; ++k)
+                    if (k < C) dst[k] = pj[k];
+                dst[C] = layout_sum<CM>(sq, C, point_rule(kind, n, N));
+                for (int k = C + 1; k < cp; ++k) dst[k] = 0.f;
+            }
         }
     }
+    if (LDSC && tid < 3) key[tid] = 0ull;
 
     // ---- serial loop
     int far = (int)start[b];
     float c[CM];
 #pragma unroll
     for (int k = 0; k < CM; ++k) c[k] = (k < C) ? P[(int64_t)far * sn + (int64_t)k * sc] : 0.f;
+    __syncthreads();
 
-    for (int i = 0; i < S; ++i) {
+    for (int i = 0;; ++i) {
         if (tid == 0) sidx[i] = far;
         if (i == S - 1) break;
 
-        unsigned bv = 0u, bi = 0xFFFFFFFFu;
-        float bc[CM];
+        // distances (two points per packed op) and the running min -- branchless
 #pragma unroll
-        for (int k = 0; k < CM; ++k) bc[k] = 0.f;
+        for (int h = 0; h < PH; ++h) {
+            pn2_f2 sq[CM];
 #pragma unroll
-        for (int j = 0; j < PPT; ++j) {
-            const int n = j * NT + tid;
-            if (n < N) {
-                float sq[CM];
-#pragma unroll
-                for (int k = 0; k < CM; ++k) {
-                    const float d = __fsub_rn(p[j][k], c[k]);
-                    sq[k] = __fmul_rn(d, d);
-                }
-                const float dd = layout_sum<CM>(sq, C, point_rule(kind, n, N));
-                const unsigned db = __float_as_uint(dd);
-                if (db < dist[j]) dist[j] = db;
-                if (j == 0 || dist[j] > bv) {
-                    bv = dist[j];
-                    bi = (unsigned)n;
-#pragma unroll
-                    for (int k = 0; k < CM; ++k) bc[k] = p[j][k];
-                }
+            for (int k = 0; k < CM; ++k) {
+                const pn2_f2 d = q[h][k] - c[k];
+                sq[k] = d * d;
             }
+            pn2_f2 dd;
+            if constexpr (FIXED && CM == 3) dd = seq_sum<CM>(sq, C);  // every rule agrees for C=3
+            else dd = layout_sum<CM>(sq, C, rule[h]);
+            // strict '<' update == min on the (non-negative) float bits; padding stays 0
+            dist[2 * h] = min(dist[2 * h], __float_as_uint(dd.x));
+            if (2 * h + 1 < PPT) dist[2 * h + 1] = min(dist[2 * h + 1], __float_as_uint(dd.y));
         }
-        // wave argmax (first index among maxima)
+        unsigned bv = dist[0];
+#pragma unroll
+        for (int j = 1; j < PPT; ++j) bv = max(bv, dist[j]);
+        // wave: max value, then its first lane (contiguous ownership -> smallest index)
         const unsigned wv = wave_max_u32(bv);
-        const unsigned wi = wave_min_u32(bv == wv ? bi : 0xFFFFFFFFu);
-        const unsigned long long own = __ballot(bi == wi);
-        const int owner = own ? (int)__builtin_ctzll(own) : 0;
-        if (NW == 1) {
+        const int ol = (int)__builtin_ctzll(__ballot(bv == wv));
+        int bj = PPT - 1;  // first owned point holding the lane's max
 #pragma unroll
-            for (int k = 0; k < CM; ++k)
-                c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bc[k]), owner));
-            far = (int)wi;
+        for (int j = PPT - 2; j >= 0; --j) bj = (dist[j] == bv) ? j : bj;
+        if constexpr (LDSC) {
+            if constexpr (NW == 1) {
+                far = ol * PPT + __builtin_amdgcn_readlane(bj, ol);
+            } else {
+                // one 64-bit LDS max per wave: key = dist bits : ~index (max dist, then first
+                // index).  key[i%3] is reset one iteration ahead; its last reader passed the
+                // previous barrier.
+                if (lane == ol) {
+                    const unsigned idx = (unsigned)(tid * PPT + bj);
+                    atomicMax(&key[i % 3], ((unsigned long long)wv << 32) | (0xFFFFFFFFu - idx));
+                }
+                if (tid == 64) key[(i + 1) % 3] = 0ull;
+                __syncthreads();
+                far = __builtin_amdgcn_readfirstlane((int)(0xFFFFFFFFu - (unsigned)key[i % 3]));
+            }
+#pragma unroll
+            for (int k = 0; k < CM; ++k) c[k] = cloud[far * CS + k];
         } else {
-            const int par = i & 1;
-            if (lane == owner) {
-                slots[par][wave][0] = __uint_as_float(wv);
-                slots[par][wave][1] = __uint_as_float(wi);
+            float bc[CM];
 #pragma unroll
-                for (int k = 0; k < CM; ++k) slots[par][wave][2 + k] = bc[k];
+            for (int k = 0; k < CM; ++k) {
+                float v = q[0][k].x;
+#pragma unroll
+                for (int j = 1; j < PPT; ++j) v = (bj == j) ? q[j >> 1][k][j & 1] : v;
+                bc[k] = v;
+            }
+            if constexpr (NW == 1) {
+                far = ol * PPT + __builtin_amdgcn_readlane(bj, ol);
+#pragma unroll
+                for (int k = 0; k < CM; ++k)
+                    c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bc[k]), ol));
+                continue;
+            }
+            const int par = i & 1;
+            if (lane == ol) {
+                float *sl = slots + (par * NW + wave) * SLOT;
+                sl[0] = __uint_as_float(wv);
+                sl[1] = __int_as_float(tid * PPT + bj);
+#pragma unroll
+                for (int k = 0; k < CM; ++k) sl[2 + k] = bc[k];
             }
             __syncthreads();
-            unsigned rv = 0u, ri = 0xFFFFFFFFu;
-            if (lane < NW) {
-                rv = __float_as_uint(slots[par][lane][0]);
-                ri = __float_as_uint(slots[par][lane][1]);
-            }
-            const unsigned gv = wave_max_u32(rv);
-            const unsigned gi = wave_min_u32(rv == gv ? ri : 0xFFFFFFFFu);
-            const unsigned long long gown = __ballot(lane < NW && ri == gi);
-            const int ow = (int)__builtin_ctzll(gown);
+            unsigned rv = 0u;
+            int ri = 0x7FFFFFFF;
+            float rc[CM];
 #pragma unroll
-            for (int k = 0; k < CM; ++k) c[k] = slots[par][ow][2 + k];
-            far = (int)gi;
+            for (int k = 0; k < CM; ++k) rc[k] = 0.f;
+            if (lane < NW) {
+                const float *sl = slots + (par * NW + lane) * SLOT;
+                rv = __float_as_uint(sl[0]);
+                ri = __float_as_int(sl[1]);
+#pragma unroll
+                for (int k = 0; k < CM; ++k) rc[k] = sl[2 + k];
+            }
+            const unsigned gv = __builtin_amdgcn_readlane(row_max_u32(rv), 0);
+            const int gw = (int)__builtin_ctzll(__ballot(lane < NW && rv == gv));
+            far = __builtin_amdgcn_readlane(ri, gw);
+#pragma unroll
+            for (int k = 0; k < CM; ++k)
+                c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rc[k]), gw));
         }
     }
     __syncthreads();
@@ -202,24 +270,49 @@ static int launch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t
                       int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx,
                       float *out_pts, float *out_packed, float *pts_packed, hipStream_t st) {
     const int kind = layout_kind(sn, sc);
-    hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED>), dim3((unsigned)B), dim3(NT), 0, st, pts,
-                       (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx, out_pts,
-                       out_packed, pts_packed, (int)pn2_packed_stride(C));
+    constexpr int NW = NT / 64;
+    constexpr int SLOT = (CM + 2 + 3) & ~3;
+    const size_t head = (size_t)((S + 3) & ~3) * 4 + 32;
+    const size_t cloud = (size_t)N * (CM == 3 ? 4 : CM) * 4;
+    const bool ldsc = cloud <= (size_t)kFpsLdsCloud && head + cloud <= (size_t)160 * 1024;
+    const size_t lds = head + (ldsc ? cloud : (size_t)2 * NW * SLOT * 4);
+    if (ldsc) {
+        static const hipError_t attr = hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&fps_kernel<NT, PPT, CM, FIXED, true>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)attr;
+        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, true>), dim3((unsigned)B), dim3(NT), lds, st, pts,
+                           (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx, out_pts,
+                           out_packed, pts_packed, (int)pn2_packed_stride(C));
+    } else {
+        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, false>), dim3((unsigned)B), dim3(NT), lds, st, pts,
+                           (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx, out_pts,
+                           out_packed, pts_packed, (int)pn2_packed_stride(C));
+    }
     PN2_LAUNCH_CHECK("fps_kernel");
     return PN2_OK;
 }
 
-// Block shape per cloud size: one wave (no barrier at all) for small clouds, a few waves for
-// mid-size ones, 1024 lanes for large ones.  CAP bounds the register-resident cloud size.
+// Block shape per cloud size.  PN2_FPS_CFG="<threads>x<points per thread>" forces one of the
+// compiled shapes (tuning experiments only).
 template <int CM, bool FIXED, int CAP>
 static int dispatch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
                         int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx,
                         float *out_pts, float *out_packed, float *pts_packed, hipStream_t st) {
 #define A pts, B, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed, st
+    int fnt = 0, fppt = 0;
+    if (const char *e = getenv("PN2_FPS_CFG")) sscanf(e, "%dx%d", &fnt, &fppt);
+#define PN2_FPS_TRY(nt, ppt) \
+    if (fnt == nt && fppt == ppt && N <= (int64_t)nt * ppt) return launch_fps<nt, ppt, CM, FIXED>(A);
+    PN2_FPS_TRY(64, 8) PN2_FPS_TRY(64, 16) PN2_FPS_TRY(128, 4) PN2_FPS_TRY(128, 8) PN2_FPS_TRY(256, 2)
+    PN2_FPS_TRY(256, 4) PN2_FPS_TRY(512, 2) PN2_FPS_TRY(1024, 1) PN2_FPS_TRY(512, 4) PN2_FPS_TRY(1024, 2)
+#undef PN2_FPS_TRY
     if (N <= 256) return launch_fps<64, 4, CM, FIXED>(A);
-    if (N <= 512) return launch_fps<64, 8, CM, FIXED>(A);
-    if (N <= 1024) return launch_fps<256, 4, CM, FIXED>(A);
-    if (N <= 2048) return launch_fps<256, 8, CM, FIXED>(A);
+    // measured on MI355X (tools/bench_fps.py): two points per lane and 4-16 waves win until
+    // the per-wave register set grows; past 2048 points the block is capped at 1024 threads
+    if (N <= 512) return launch_fps<256, 2, CM, FIXED>(A);
+    if (N <= 1024) return launch_fps<512, 2, CM, FIXED>(A);
+    if (N <= 2048) return launch_fps<1024, 2, CM, FIXED>(A);
     if (N <= 4096) return launch_fps<1024, 4, CM, FIXED>(A);
     if constexpr (CAP >= 8192)
         if (N <= 8192) return launch_fps<1024, 8, CM, FIXED>(A);

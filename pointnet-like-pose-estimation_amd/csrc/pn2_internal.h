@@ -35,49 +35,56 @@ constexpr int kMaxC = 16;  // point dims (xyz + one-hot) held in registers
 //                            scalar tail first, then tail+v0+...+v7.
 //  strided (stride_n == 1):  n < 16*floor(N/16) -> sequential; tail -> row_sum order.
 // `a` is a register array; C is runtime (<= CM).
-template <int CM>
-__device__ __forceinline__ float seq_sum(const float (&a)[CM], int C) {
-    float r = 0.f;
+// Element-wise adds in round-to-nearest.  The vector overload (two points per packed
+// v_pk_add_f32) relies on -ffp-contract=off in the translation units that use it.
+typedef float pn2_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ pn2_f2 add_rn(pn2_f2 a, pn2_f2 b) { return a + b; }
+
+template <int CM, typename T>
+__device__ __forceinline__ T seq_sum(const T (&a)[CM], int C) {
+    T r = T(0.f);
 #pragma unroll
     for (int k = 0; k < CM; ++k)
-        if (k < C) r = __fadd_rn(r, a[k]);
+        if (k < C) r = add_rn(r, a[k]);
     return r;
 }
 
-template <int CM>
-__device__ __forceinline__ float rowsum4(const float (&a)[CM], int C) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+template <int CM, typename T>
+__device__ __forceinline__ T rowsum4(const T (&a)[CM], int C) {
+    T acc[4] = {T(0.f), T(0.f), T(0.f), T(0.f)};
     const int n4 = (C / 4) * 4;
 #pragma unroll
     for (int k = 0; k < CM; ++k) {
-        if (k < n4) acc[k & 3] = __fadd_rn(acc[k & 3], a[k]);
-        else if (k < C) acc[0] = __fadd_rn(acc[0], a[k]);
+        if (k < n4) acc[k & 3] = add_rn(acc[k & 3], a[k]);
+        else if (k < C) acc[0] = add_rn(acc[0], a[k]);
     }
-    return __fadd_rn(__fadd_rn(__fadd_rn(acc[0], acc[1]), acc[2]), acc[3]);
+    return add_rn(add_rn(add_rn(acc[0], acc[1]), acc[2]), acc[3]);
 }
 
-template <int CM>
-__device__ __forceinline__ float contig_sum(const float (&a)[CM], int C) {
+template <int CM, typename T>
+__device__ __forceinline__ T contig_sum(const T (&a)[CM], int C) {
     if (C < 8) return rowsum4<CM>(a, C);
     const int nv8 = (C / 8) * 8;
-    float v[8];
+    T v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = 0.f;
-#pragma unroll
-    for (int k = 0; k < CM; ++k)
-        if (k < nv8) v[k & 7] = __fadd_rn(v[k & 7], a[k]);
-    float r = 0.f;
+    for (int k = 0; k < 8; ++k) v[k] = T(0.f);
 #pragma unroll
     for (int k = 0; k < CM; ++k)
-        if (k >= nv8 && k < C) r = __fadd_rn(r, a[k]);
+        if (k < nv8) v[k & 7] = add_rn(v[k & 7], a[k]);
+    T r = T(0.f);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) r = __fadd_rn(r, v[k]);
+    for (int k = 0; k < CM; ++k)
+        if (k >= nv8 && k < C) r = add_rn(r, a[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r = add_rn(r, v[k]);
     return r;
 }
 
-// rule: 0 = contig, 1 = strided sequential region, 2 = strided tail (row_sum)
-template <int CM>
-__device__ __forceinline__ float layout_sum(const float (&a)[CM], int C, int rule) {
+// sum of squares of one row in the order ATen uses for its layout/position (rule: 0 contiguous,
+// 1 strided sequential, 2 strided tail)
+template <int CM, typename T>
+__device__ __forceinline__ T layout_sum(const T (&a)[CM], int C, int rule) {
     if (rule == 0) return contig_sum<CM>(a, C);
     if (rule == 1) return seq_sum<CM>(a, C);
     return rowsum4<CM>(a, C);

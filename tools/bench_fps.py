@@ -1,0 +1,68 @@
+"""Sweep the FPS kernel's block shapes (PN2_FPS_CFG) on the GPU for the BASELINE geometries,
+checking every variant against the CPU oracle first.  Prints one line per (shape, variant):
+microseconds per launch and per serial iteration."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "pointnet-like-pose-estimation_amd"), os.path.join(ROOT, "tests", "golden")):
+    sys.path.insert(0, p)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import cases  # noqa: E402
+import oracle  # noqa: E402
+import pn2  # noqa: E402
+
+SHAPES = [  # (name, B, N, C, S, kind)
+    ("ssg_sa1", 32, 1024, 3, 512, "uniform3"),
+    ("ssg_sa2", 32, 512, 3, 128, "uniform3"),
+    ("msg_sa1", 32, 4096, 3, 512, "uniform3"),
+    ("pose_sa1", 64, 2048, 10, 512, "onehot10"),
+    ("pose_sa2", 64, 512, 10, 128, "onehot10"),
+    ("stress_sa1", 128, 16384, 3, 512, "uniform3"),
+]
+VARIANTS = ["64x4", "64x8", "64x16", "128x4", "128x8", "256x2", "256x4", "512x2", "512x4", "1024x1",
+            "1024x2", "1024x4", "1024x8", "1024x16", ""]
+
+
+def main():
+    dev = torch.device("cuda")
+    res = []
+    for name, B, N, C, S, kind in SHAPES:
+        x = cases.as_layout(cases.cloud(kind, B, N, 5), "strided")
+        xd = x.permute(0, 2, 1).contiguous().to(dev).permute(0, 2, 1)
+        start = torch.randint(0, N, (B,), generator=torch.Generator().manual_seed(1))
+        sd = start.to(dev)
+        want = oracle.farthest_point_sample(x[:2], S, start[:2])
+        for v in VARIANTS:
+            if v:
+                nt, ppt = map(int, v.split("x"))
+                if nt * ppt < N or nt * ppt >= 4 * N:
+                    continue
+            os.environ["PN2_FPS_CFG"] = v
+            try:
+                idx = torch.ops.pn2.fps(xd, S, sd)[0]
+            except Exception as e:  # variant not compiled for this C
+                continue
+            ok = bool((idx[:2].cpu().numpy() == want).all())
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 5
+            e0.record()
+            for _ in range(reps):
+                torch.ops.pn2.fps(xd, S, sd)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
+            r = {"shape": name, "variant": v or "default", "us": round(us, 1), "us_per_iter": round(us / S, 3), "exact": ok}
+            print(json.dumps(r), flush=True)
+            res.append(r)
+    os.environ.pop("PN2_FPS_CFG", None)
+    with open(os.path.join(ROOT, "gpurun_out", "fps_sweep.json"), "w") as fh:
+        json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
