@@ -6,11 +6,17 @@ of N=1024 points per GPU, on the MI355X-native SA path.
 
 One step = one forward of the head over every rank's batch shard (weak scaling: B clouds per
 GPU, global batch = B*N) followed by the RCCL all_gather of the logits -- the only exchange the
-data-parallel path has.  Inputs are resident in HBM before the timed region.  Rank 0 prints one
-JSON line (contract in the task statement) with:
+data-parallel path has.  The forward runs op by op (--graph replays it as a HIP graph via
+pn2.graphs.GraphedForward: same kernels and CPU-RNG draws; measured slower on MI355X, see
+DESIGN.md).  Inputs are resident in HBM before the timed region, which carries no
+instrumentation.  Rank 0 prints one JSON line (contract in the task statement) with:
+  value         clouds/s of the timed region; with --graph, eager_value is the same K steps op
+                by op.
   roofline      dominant kernel = pn2_sa_mlp_max_f32 (the fused gather+MLP+max, fp32 MFMA):
                 achieved = algorithmic FLOPs (2*M*sum(cin*cout) per launch, cin unpadded) /
-                HIP-event-timed launch duration on the launch stream, over the timed steps;
+                launch duration timed with HIP events on the launch stream, over a further
+                K eager steps (events cannot sit between the nodes of a replayed graph; kernel
+                durations are launch-mode independent -- profiles/ has the rocprofv3 check);
                 peak = 157.3 TFLOP/s (gfx950 dense fp32 MFMA).  traffic = HBM bytes per launch
                 from rocprofv3 PMC (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE, per
                 MI355X_MICROARCH.md) when present for this config, else null.
@@ -54,6 +60,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline sample")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="replay the forward as a HIP graph")
     return ap.parse_args()
 
 
@@ -82,6 +89,8 @@ def make_inputs(cfg, B, lo, dev, rank):
 
 
 def step(names, models, x, mean, gB, lo):
+    """One forward of every head over this rank's shard + the logits all_gather.  `models` are
+    nn.Modules (eager) or pn2.graphs.GraphedForward wrappers."""
     from pn2 import shard
     outs = []
     with torch.no_grad(), shard.batch_shard(gB, lo):
@@ -156,15 +165,17 @@ def main():
     head, B, N, kind, desc = CONFIGS[a.config]
     gB = B * world
     lo, hi = shard.shard_range(gB, rank, world)
-    names, models = build_models(a.config, dev)
+    names, eager_models = build_models(a.config, dev)
+    from pn2.graphs import GraphedForward
+    models = [GraphedForward(m) for m in eager_models] if a.graph else eager_models
     x, mean = make_inputs(a.config, hi - lo, lo, dev, rank)
     torch.manual_seed(1234)  # identical CPU RNG stream on every rank (FPS start draws)
 
-    for _ in range(a.warmup):
+    for _ in range(max(a.warmup, 2) if a.graph else a.warmup):  # graph: 1st call captures
         step(names, models, x, mean, gB, lo)
     torch.cuda.synchronize()
 
-    def timed(k, timer):
+    def timed(k, timer, models=models):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -184,13 +195,23 @@ def main():
             dist.barrier()
         return el, kt
 
-    el, kt = timed(a.steps, not a.no_kernel_timer)
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
+    def max_over_ranks(el):
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    el, _ = timed(a.steps, False)
+    el = max_over_ranks(el)
     ms = el / a.steps * 1e3
     value = gB * a.steps / el
+    eager_value = value
+    if a.graph:
+        el_e, _ = timed(a.steps, False, eager_models)
+        eager_value = gB * a.steps / max_over_ranks(el_e)
+    kt = None
+    if not a.no_kernel_timer:
+        _, kt = timed(a.steps, True, eager_models)
 
     kern = kt.summary() if kt is not None else {}
     mlp = kern.get("pn2_sa_mlp_max_f32")
@@ -221,6 +242,7 @@ def main():
             "config": {"workload": desc, "global_batch": gB, "points": N, "heads": names,
                        "parallelism": "dp%d" % world},
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+            "launch": "hip_graph" if a.graph else "eager", "eager_value": round(eager_value, 2),
         }
         print(json.dumps(line))
     if world > 1:

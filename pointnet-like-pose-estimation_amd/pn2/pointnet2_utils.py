@@ -5,7 +5,9 @@ the reference, so its heads (pointnet2_cls_ssg/msg, rotation_/translation_/sign_
 unchanged when this module is importable as ``pointnet2_utils`` (see the shim
 ``pointnet-like-pose-estimation_amd/pointnet2_utils.py``).
 
-Eval-mode inference (``model.eval()`` / no autograd) of an SA layer is three HIP launches:
+Eval-mode inference (``model.eval()`` / no autograd) of an SA layer is three HIP launches
+(FPS and ball query on the geometry stream, see geometry.py, overlapping the previous layer's
+MLP):
   pn2::fps            FPS + gathered centroids + packed (coords, ssq) records
   pn2::ball_query     first-K-in-radius neighbour indices
   pn2::sa_mlp_max_    fused gather -> conv1x1/BN/ReLU chain -> max over neighbours
@@ -24,6 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from . import geometry
 from . import ops
 from . import shard
 
@@ -32,7 +35,7 @@ from . import shard
 def _draw_start(B, N, device):
     """The reference's FPS start draw: torch.randint(0, N, (B,), dtype=long) on the CPU default
     generator (pointnet2_utils.py:59) -- one draw per FPS call, sliced when sharded."""
-    return shard.draw_start(B, N).to(device, non_blocking=True)
+    return shard.device_start(B, N, device)
 
 
 def _channels_last(feature):
@@ -179,8 +182,10 @@ class PointNetSetAbstraction(nn.Module):
             new_points = torch.zeros(B, C, 1, device=dev, dtype=torch.float32)
             return new_points, out.view(B, 1, cout).permute(0, 2, 1)
         S, K = self.point_number, self.sample_number
-        _, new_points, cpk, ppk = ops.fps(pts, S, _draw_start(B, N, dev))
-        idx = ops.ball_query(ppk, cpk, C, self.radius, K)
+        with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
+            _, new_points, cpk, ppk = ops.fps(pts, S, _draw_start(B, N, dev))
+            idx = ops.ball_query(ppk, cpk, C, self.radius, K)
+        span.finish([new_points], [new_points, idx])
         out = torch.empty(B * S, cout, device=dev, dtype=torch.float32)
         ops.sa_mlp_max_(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
                         cins)
@@ -235,13 +240,16 @@ class PointNetSetAbstractionMsg(nn.Module):
         chains = [_pack_chain(self.conv_blocks[i], self.bn_blocks[i], self._pack_cache[i], 0)
                   for i in range(len(self.radius_list))]
         total = sum(ch[0][-1].shape[1] for ch in chains)
-        _, new_points, cpk, ppk = ops.fps(pts, S, _draw_start(B, N, dev))
+        with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
+            _, new_points, cpk, ppk = ops.fps(pts, S, _draw_start(B, N, dev))
+            idxs = [ops.ball_query(ppk, cpk, C, r, k)
+                    for r, k in zip(self.radius_list, self.sample_number_list)]
+        span.finish([new_points], [new_points] + idxs)
         out = torch.empty(B * S, total, device=dev, dtype=torch.float32)
         col = 0
-        for i, radius in enumerate(self.radius_list):
+        for i, idx in enumerate(idxs):
             wts, als, bes, cins = chains[i]
             cout = wts[-1].shape[1]
-            idx = ops.ball_query(ppk, cpk, C, radius, self.sample_number_list[i])
             ops.sa_mlp_max_(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
                             new_points, idx, wts, als, bes, cins)
             col += cout

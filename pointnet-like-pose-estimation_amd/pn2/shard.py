@@ -47,6 +47,27 @@ def draw_start(B, N):
     return t.pin_memory() if torch.cuda.is_available() else t
 
 
+def device_start(B, N, device):
+    """The FPS start draw as a device tensor.  Inside a graph capture (graphs.GraphedForward)
+    the draw is not taken here: the capture reads a static device slot that every replay
+    refills with a fresh draw, taken in the same order as the eager forward takes them."""
+    rec = getattr(_state, "graph", None)
+    if rec is not None:
+        return rec(B, N, device)
+    return draw_start(B, N).to(device, non_blocking=True)
+
+
+@contextlib.contextmanager
+def start_source(fn):
+    """Route device_start(B, N, device) to fn for the duration (graph record/capture)."""
+    prev = getattr(_state, "graph", None)
+    _state.graph = fn
+    try:
+        yield
+    finally:
+        _state.graph = prev
+
+
 def shard_range(global_batch, rank, world):
     """Contiguous [lo, hi) of clouds owned by `rank` (the remainder goes to the first ranks)."""
     base, rem = divmod(global_batch, world)

@@ -187,3 +187,84 @@ def test_stress_config_geometry():
     first = q[:, :, :1]
     d_ = np.diff(q, axis=-1)
     assert ((d_ > 0) | ((d_ <= 0) & (q[:, :, 1:] == first))).all()
+
+
+@pytest.mark.parametrize("head", ["ClsSSG", "ClsMSG"])
+def test_geometry_stream_matches_single_stream(head, monkeypatch):
+    """FPS/ball query on the geometry stream (overlapping the previous layer's MLP) give the
+    same bits as running everything on the caller's stream -- over back-to-back forwards whose
+    temporaries churn the caching allocator, with the inputs freed right after each launch."""
+    from pn2 import heads as H
+    torch.manual_seed(4)
+    model = getattr(H, head)().eval()
+    cases.randomize_bn(model, 4)
+    model = model.to(DEV)
+    B, N = (16, 1024) if head == "ClsSSG" else (8, 2048)
+    clouds = [cases.cloud("uniform3", B, N, 60 + i).permute(0, 2, 1).contiguous() for i in range(4)]
+
+    def run():
+        torch.manual_seed(9)
+        outs = []
+        with torch.no_grad():
+            for c in clouds:
+                x = c.to(DEV, non_blocking=True)
+                outs.append(model(x)[0])
+                del x
+        torch.cuda.synchronize()
+        return [o.cpu().numpy() for o in outs]
+
+    monkeypatch.setenv("PN2_GEOMETRY_STREAM", "0")
+    want = run()
+    monkeypatch.setenv("PN2_GEOMETRY_STREAM", "1")
+    for _ in range(2):
+        got = run()
+        for g, w in zip(got, want):
+            np.testing.assert_array_equal(g, w)
+
+
+@pytest.mark.parametrize("head", ["ClsSSG", "ClsMSG", "RotationSSG"])
+def test_graph_replay_matches_eager(head):
+    """GraphedForward: the first call runs eagerly and captures; replays give the eager bits for
+    new inputs, take the FPS start draws from the CPU generator in the eager order (the RNG is
+    left in the same state), follow shard.batch_shard slicing, and re-capture after an
+    in-place parameter update."""
+    from pn2 import heads as H
+    from pn2 import shard
+    from pn2.graphs import GraphedForward
+    torch.manual_seed(6)
+    model = getattr(H, head)().eval()
+    cases.randomize_bn(model, 6)
+    model = model.to(DEV)
+    kind = "onehot10" if head.startswith("Rotation") else "uniform3"
+    B, N = (8, 2048) if head == "ClsMSG" else (16, 1024)
+    xs = [cases.cloud(kind, B, N, 80 + i).permute(0, 2, 1).contiguous().to(DEV) for i in range(4)]
+
+    def first(o):
+        return (o[0] if isinstance(o, tuple) else o).clone()
+
+    def run(fn):
+        torch.manual_seed(21)
+        outs = []
+        with torch.no_grad():
+            for i, x in enumerate(xs):
+                if i == 2:  # sharded call: second half of a 2*B global batch
+                    with shard.batch_shard(2 * B, B):
+                        outs.append(first(fn(x)))
+                else:
+                    outs.append(first(fn(x)))
+            if head == "ClsSSG":  # in-place parameter change -> recapture
+                rm = model.sa1.mlp_bns[0].running_mean
+                saved = rm.clone()
+                rm.add_(0.25)
+                outs.append(first(fn(xs[0])))
+                outs.append(first(fn(xs[1])))
+                rm.copy_(saved)
+        return [o.cpu().numpy() for o in outs], torch.randint(0, 1 << 30, (4,))
+
+    want, rng_want = run(model)
+    gm = GraphedForward(model)
+    got, rng_got = run(gm)
+    assert gm._graph is not None
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+    np.testing.assert_array_equal(rng_got.numpy(), rng_want.numpy())

@@ -12,7 +12,7 @@ ok() { local rc=$1 what=$2; echo "[gpu_check] $what rc=$rc"; if [ $rc -ne 0 ] &&
 for s in $STEPS; do
   case $s in
     pytest)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -rf --timeout=600 ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1; ok $? pytest
+      timeout -k 10 900 python -m pytest tests -m gpu -q -rf --timeout=600 ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1; ok $? pytest
       tail -30 $OUT/pytest_gpu.log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; ok $? smoke
