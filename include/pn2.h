@@ -56,7 +56,8 @@ int64_t pn2_packed_stride(int64_t C);
  *   out_pts    [B,S,C] float32 contiguous, or NULL   index_points(points, fps_idx)
  *   out_packed [B,S,cp] float32, or NULL         packed centroids (contiguous-layout ssq)
  *   pts_packed [B,N,cp] float32, or NULL         packed input points (input-layout ssq)
- * Requires N <= 32768 and C <= 16. */
+ * The cloud is register-resident: N <= 16384 for C == 3, N <= 8192 for C == 10, N <= 4096 for
+ * other C <= 16 (else PN2_EUNSUPPORTED); S <= 8192. */
 int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
                 int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
                 float *out_packed, float *pts_packed, void *stream);
