@@ -40,7 +40,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 1
+#define PN2_ABI_VERSION 2
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -119,7 +119,19 @@ typedef struct pn2_mlp_layer {
     const float *beta;  /* [cout] */
     int64_t cin;
     int64_t cout;
+    const void *wt_split; /* pn2_pack_layer_split_bf16 image of the same W (same rot), or NULL */
 } pn2_mlp_layer;
+
+/* The same W packed for the split-bf16 chain kernel: three bf16 planes (hi, mid, lo with
+ * W = hi + mid + lo to 2^-24 relative), each [cout/32][ceil(cin/16)][64 lanes][8] in MFMA
+ * fragment order (lane 32h + r, element j holds W[32t + r][(k + rot) % cin], k = 16kb +
+ * (j&3) + 8(j>>2) + 4h; 0 past cin).  pn2_layer_split_bytes(cout, cin) bytes, 16-byte aligned.
+ * Chains given wt_split for every layer (3 layers, grouped rows, hidden widths 32..128) run as
+ * one register-resident kernel with fp32-accurate 6-product bf16 MFMA arithmetic; others (and
+ * PN2_MLP_PATH=f32) use the fp32 MFMA kernels. */
+int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin);
+int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t rot, void *out,
+                              void *stream);
 
 typedef struct pn2_sa_src {
     int mode; /* PN2_SRC_* */
@@ -147,6 +159,12 @@ int64_t pn2_sa_mlp_workspace_bytes(const pn2_sa_src *src, const pn2_mlp_layer *l
 int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers, int nlayers,
                        int pool, float *out, int64_t ostride, float *workspace,
                        int64_t workspace_bytes, void *stream);
+
+/* Which kernel family served this thread's last successful pn2_sa_mlp_max_f32 call:
+ * PN2_PATH_F32 (fp32 MFMA kernels) or PN2_PATH_SPLIT_BF16 (register-resident chain). */
+#define PN2_PATH_F32 1
+#define PN2_PATH_SPLIT_BF16 2
+int pn2_sa_mlp_last_path(void);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,10 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
 
 constexpr int kMaxC = 16;  // point dims (xyz + one-hot) held in registers
 
+// sa_chain.hip: 1 launched, 0 not eligible, <0 error
+int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
+                     float *out, int64_t ostride, int64_t M, int64_t K, hipStream_t st);
+
 // --------------------------------------------------------------- device: reference sum orders
 // torch.sum(x**2, -1) over the channel axis, reproduced bit-for-bit (torch 2.10 CPU, AVX512);
 // pinned in oracle/pn2_oracle.c and tests/test_oracle_golden.py.

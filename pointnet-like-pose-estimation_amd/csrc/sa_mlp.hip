@@ -862,6 +862,9 @@ static int run_plan(const pn2_sa_src &cur, const pn2_mlp_layer *layers, int l0, 
     return PN2_OK;
 }
 
+static thread_local int g_last_path = 0;
+extern "C" int pn2_sa_mlp_last_path(void) { return g_last_path; }
+
 extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers,
                                   int nlayers, int pool, float *out, int64_t ostride,
                                   float *workspace, int64_t workspace_bytes, void *stream) {
@@ -873,6 +876,12 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
     if (M == 0) return PN2_OK;
     if (pool) PN2_REQUIRE(M % K == 0, "pn2_sa_mlp_max_f32: rows not a multiple of the group size");
     hipStream_t st = as_stream(stream);
+    rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, st);
+    if (rc != 0) {
+        if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
+        return rc < 0 ? rc : PN2_OK;
+    }
+    g_last_path = PN2_PATH_F32;
     const int64_t w = workspace_width(*src, layers, nlayers, M, K);
     if (w > 0)
         PN2_REQUIRE(workspace && workspace_bytes >= 2 * M * w * 4 && ((uintptr_t)workspace & 15) == 0,

@@ -26,7 +26,8 @@ class Pn2Error(RuntimeError):
 
 
 class MlpLayer(ctypes.Structure):
-    _fields_ = [("wt", _vp), ("alpha", _vp), ("beta", _vp), ("cin", _i64), ("cout", _i64)]
+    _fields_ = [("wt", _vp), ("alpha", _vp), ("beta", _vp), ("cin", _i64), ("cout", _i64),
+                ("wt_split", _vp)]
 
 
 class SaSrc(ctypes.Structure):
@@ -45,6 +46,8 @@ SRC_GROUP_XYZ_FIRST = 0
 SRC_GROUP_FEAT_FIRST = 1
 SRC_GROUP_ALL = 2
 SRC_ROWS = 3
+PATH_F32 = 1
+PATH_SPLIT_BF16 = 2
 
 # name -> (restype, argtypes); every symbol include/pn2.h declares
 SIGNATURES = {
@@ -60,12 +63,15 @@ SIGNATURES = {
                              _vp, _i64, _vp, _i64, _int, _vp, _vp]),
     "pn2_layer_cin_pad": (_i64, [_i64]),
     "pn2_pack_layer_f32": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _dbl, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "pn2_layer_split_bytes": (_i64, [_i64, _i64]),
+    "pn2_sa_mlp_last_path": (_int, []),
+    "pn2_pack_layer_split_bf16": (_int, [_vp, _i64, _i64, _i64, _vp, _vp]),
     "pn2_sa_mlp_workspace_bytes": (_i64, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int]),
     "pn2_sa_mlp_max_f32": (_int, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int, _int, _vp,
                                   _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _lib = None
 
 

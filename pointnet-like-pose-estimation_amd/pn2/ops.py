@@ -268,6 +268,29 @@ def _(weight, bias, gamma, beta, mean, var, eps, rot):
     return e(cin_pad(cin) // 2, cout, 2), e(cout), e(cout)
 
 
+@torch.library.custom_op("pn2::pack_layer_split", mutates_args=())
+def pack_layer_split(weight: Tensor, rot: int) -> Tensor:
+    """Conv2d 1x1 weight [cout,cin,1,1] -> the split-bf16 image of pn2_pack_layer_split_bf16
+    (three bf16 planes hi/mid/lo in MFMA fragment order, same `rot` as pack_layer), flat
+    bfloat16.  Used by the register-resident chain kernel (sa_chain.hip)."""
+    _dev(weight, "pn2::pack_layer_split")
+    cout, cin = weight.shape[0], weight.shape[1]
+    w = weight.reshape(cout, cin).contiguous()
+    nbytes = int(_L.pn2_layer_split_bytes(cout, cin))
+    if nbytes < 0:
+        raise ValueError("pn2::pack_layer_split: cout=%d must be a positive multiple of 32" % cout)
+    out = torch.empty(nbytes // 2, dtype=torch.bfloat16, device=weight.device)
+    _run("pn2_pack_layer_split_bf16", _L.pn2_pack_layer_split_bf16,
+         (w.data_ptr(), cout, cin, int(rot), out.data_ptr(), _stream(weight)), weight.device)
+    return out
+
+
+@pack_layer_split.register_fake
+def _(weight, rot):
+    cout, cin = weight.shape[0], weight.shape[1]
+    return weight.new_empty(3 * cout * ((cin + 15) // 16) * 16, dtype=torch.bfloat16)
+
+
 # ------------------------------------------------------------------------------ sa_mlp_max_
 def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K):
     s = SaSrc()
@@ -294,10 +317,12 @@ def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K):
 @torch.library.custom_op("pn2::sa_mlp_max_", mutates_args=("out",))
 def sa_mlp_max_(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor],
                 centers: Optional[Tensor], idx: Optional[Tensor], wts: List[Tensor],
-                alphas: List[Tensor], betas: List[Tensor], cins: List[int]) -> None:
+                alphas: List[Tensor], betas: List[Tensor], cins: List[int],
+                splits: List[Tensor]) -> None:
     """Fused gather -> MLP (conv1x1+BN+ReLU)* -> max over each group, written channels-last
     into `out` ([G, >=cout] view with unit column stride; G = B*S groups, or B for
-    group_all).  mode: 0 SSG grouping, 1 MSG grouping, 2 group_all."""
+    group_all).  mode: 0 SSG grouping, 1 MSG grouping, 2 group_all.  splits: the
+    pack_layer_split images of the same layers (empty list: fp32 kernels only)."""
     _dev(points, "pn2::sa_mlp_max_")
     B, N, C = points.shape
     D = 0 if feature is None else feature.shape[2]
@@ -316,6 +341,7 @@ def sa_mlp_max_(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor
         layers[i].beta = betas[i].data_ptr()
         layers[i].cin = cins[i]
         layers[i].cout = wts[i].shape[1]  # [cin_pad/2, cout, 2]
+        layers[i].wt_split = splits[i].data_ptr() if splits else 0
     if out.stride(-1) != 1:
         raise ValueError("pn2::sa_mlp_max_: out must have unit column stride")
     ws_bytes = int(_L.pn2_sa_mlp_workspace_bytes(src, layers, n))
@@ -330,5 +356,5 @@ def sa_mlp_max_(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor
 
 
 @sa_mlp_max_.register_fake
-def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins):
+def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits):
     return None

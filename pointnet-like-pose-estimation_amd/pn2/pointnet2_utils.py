@@ -62,18 +62,19 @@ def _pack_chain(convs, bns, cache, rot0):
         tensors += [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
     key = (rot0,) + tuple((None if t is None else (t.data_ptr(), t._version)) for t in tensors)
     if cache.get("key") != key:
-        wts, als, bes, cins = [], [], [], []
+        wts, als, bes, cins, splits = [], [], [], [], []
         with torch.no_grad():
             for li, (conv, bn) in enumerate(zip(convs, bns)):
+                rot = rot0 if li == 0 else 0
                 wt, al, be = ops.pack_layer(conv.weight, conv.bias, bn.weight, bn.bias,
-                                            bn.running_mean, bn.running_var, float(bn.eps),
-                                            rot0 if li == 0 else 0)
+                                            bn.running_mean, bn.running_var, float(bn.eps), rot)
                 wts.append(wt)
                 als.append(al)
                 bes.append(be)
                 cins.append(conv.weight.shape[1])
+                splits.append(ops.pack_layer_split(conv.weight, rot))
         cache["key"] = key
-        cache["layers"] = (wts, als, bes, cins)
+        cache["layers"] = (wts, als, bes, cins, splits)
     return cache["layers"]
 
 
@@ -173,12 +174,13 @@ class PointNetSetAbstraction(nn.Module):
         B, N, C = pts.shape
         # reference row order is [xyz, feature] (:114, :139); kernels use [feature, xyz]
         rot0 = C if feat is not None else 0
-        wts, als, bes, cins = _pack_chain(self.mlp_convs, self.mlp_bns, self._pack_cache, rot0)
+        wts, als, bes, cins, splits = _pack_chain(self.mlp_convs, self.mlp_bns, self._pack_cache, rot0)
         cout = wts[-1].shape[1]
         dev = pts.device
         if self.group_all:
             out = torch.empty(B, cout, device=dev, dtype=torch.float32)
-            ops.sa_mlp_max_(out, _lib.SRC_GROUP_ALL, pts, feat, None, None, wts, als, bes, cins)
+            ops.sa_mlp_max_(out, _lib.SRC_GROUP_ALL, pts, feat, None, None, wts, als, bes, cins,
+                            splits)
             new_points = torch.zeros(B, C, 1, device=dev, dtype=torch.float32)
             return new_points, out.view(B, 1, cout).permute(0, 2, 1)
         S, K = self.point_number, self.sample_number
@@ -188,7 +190,7 @@ class PointNetSetAbstraction(nn.Module):
         span.finish([new_points], [new_points, idx])
         out = torch.empty(B * S, cout, device=dev, dtype=torch.float32)
         ops.sa_mlp_max_(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
-                        cins)
+                        cins, splits)
         return new_points.permute(0, 2, 1), out.view(B, S, cout).permute(0, 2, 1)
 
     def _forward_autograd(self, points, feature):
@@ -248,10 +250,10 @@ class PointNetSetAbstractionMsg(nn.Module):
         out = torch.empty(B * S, total, device=dev, dtype=torch.float32)
         col = 0
         for i, idx in enumerate(idxs):
-            wts, als, bes, cins = chains[i]
+            wts, als, bes, cins, splits = chains[i]
             cout = wts[-1].shape[1]
             ops.sa_mlp_max_(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
-                            new_points, idx, wts, als, bes, cins)
+                            new_points, idx, wts, als, bes, cins, splits)
             col += cout
         return new_points.permute(0, 2, 1), out.view(B, S, total).permute(0, 2, 1)
 

@@ -1,0 +1,90 @@
+"""GPU parity of the grouped MLP + max (pn2_sa_mlp_max_f32 through the SA modules) against the
+float64 oracle (oracle.mlp_max, pointnet2_utils.py:167-172 / 211-218), for both kernel
+families: the split-bf16 register-resident chain (sa_chain.hip, default) and the fp32 MFMA
+kernels (PN2_MLP_PATH=f32).  Cases cover every pooling mode of both (K = 8, 16, 32 in
+registers; 64, 128 in LDS; 96 through HBM atomics), features absent / unaligned / aligned,
+C = 3 and the 10-channel pose layout, SSG and MSG row orders, and a width chain with no chain
+signature (served by the fp32 kernels).  Tolerance as test_gpu_sa.py: 1e-5 relative + 1e-5 of
+the output's max magnitude."""
+import numpy as np
+import pytest
+import torch
+
+import cases
+import oracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (C, D, K, S, N, mlp, msg, chain kernel expected)
+CASES = [
+    (3, 0, 32, 64, 512, [64, 64, 128], False, True),      # SSG sa1 shape
+    (3, 64, 64, 32, 256, [128, 128, 256], False, True),   # SSG sa2 shape, LDS pool
+    (3, 13, 16, 32, 256, [32, 32, 64], True, True),       # MSG, unaligned D, K=16
+    (3, 8, 8, 40, 256, [64, 96, 128], True, True),        # K=8
+    (10, 0, 128, 16, 512, [64, 64, 128], False, True),    # pose layout, K=128
+    (3, 4, 96, 8, 256, [64, 64, 128], False, True),       # K=96: HBM atomics
+    (3, 16, 32, 16, 256, [96, 64, 64], False, False),     # no chain signature -> fp32
+    (3, 0, 32, 8, 128, [64, 128], False, False),          # 2 layers -> fp32
+]
+
+
+def _close(got, want, rtol=1e-5):
+    got = np.asarray(got, np.float64)
+    want = np.asarray(want, np.float64)
+    atol = rtol * max(float(np.abs(want).max()), 1e-30)
+    np.testing.assert_allclose(got, want, rtol=rtol, atol=atol)
+
+
+def _oracle_layers(convs, bns):
+    out = []
+    for conv, bn in zip(convs, bns):
+        out.append(dict(W=conv.weight.detach().reshape(conv.weight.shape[0], -1).cpu().numpy(),
+                        b=conv.bias.detach().cpu().numpy(), gamma=bn.weight.detach().cpu().numpy(),
+                        beta=bn.bias.detach().cpu().numpy(), mean=bn.running_mean.cpu().numpy(),
+                        var=bn.running_var.cpu().numpy(), eps=bn.eps))
+    return out
+
+
+@pytest.mark.parametrize("path", ["chain", "f32"])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_sa_mlp_vs_oracle(case, path, monkeypatch):
+    import pn2
+    from pn2 import _lib
+    C, D, K, S, N, mlp, msg, chain_ok = CASES[case]
+    if path == "f32":
+        monkeypatch.setenv("PN2_MLP_PATH", "f32")
+    else:
+        monkeypatch.delenv("PN2_MLP_PATH", raising=False)
+    B, radius = 2, 0.35
+    pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 100 + case)
+    gen = torch.Generator().manual_seed(200 + case)
+    feat = torch.randn(B, N, D, generator=gen) if D else None
+    torch.manual_seed(case)
+    if msg:
+        sa = pn2.PointNetSetAbstractionMsg(S, [K], [radius], D, [mlp])
+        convs, bns = sa.conv_blocks[0], sa.bn_blocks[0]
+    else:
+        sa = pn2.PointNetSetAbstraction(S, K, radius, C + D, mlp)
+        convs, bns = sa.mlp_convs, sa.mlp_bns
+    cases.randomize_bn(sa, case)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous()
+    f = feat.permute(0, 2, 1).contiguous() if D else None
+    torch.manual_seed(1000 + case)
+    with torch.no_grad():
+        newp, newf = sa(x.to(DEV), None if f is None else f.to(DEV))
+    torch.cuda.synchronize()
+    want_path = _lib.PATH_SPLIT_BF16 if (chain_ok and path == "chain") else _lib.PATH_F32
+    assert _lib.load().pn2_sa_mlp_last_path() == want_path
+
+    ps = x.permute(0, 2, 1)  # the module's own (point-contiguous) view
+    torch.manual_seed(1000 + case)
+    start = torch.randint(0, N, (B,), dtype=torch.long)
+    fi = oracle.farthest_point_sample(ps, S, start)
+    ctr = oracle.index_points(ps, fi)
+    np.testing.assert_array_equal(newp.permute(0, 2, 1).cpu().numpy(), ctr)
+    idx = oracle.query_ball_point(radius, K, ps, ctr)
+    grouped = oracle.group(ps, feat, idx, ctr, feature_first=msg)
+    want = oracle.mlp_max(grouped, _oracle_layers(convs, bns))
+    _close(newf.permute(0, 2, 1).cpu().numpy(), want)
