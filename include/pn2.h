@@ -119,19 +119,25 @@ typedef struct pn2_mlp_layer {
     const float *beta;  /* [cout] */
     int64_t cin;
     int64_t cout;
-    const void *wt_split; /* pn2_pack_layer_split_bf16 image of the same W (same rot), or NULL */
+    const void *wt_split; /* pn2_pack_layer_split_bf16 image of the same W, or NULL */
 } pn2_mlp_layer;
 
 /* The same W packed for the split-bf16 chain kernel: three bf16 planes (hi, mid, lo with
- * W = hi + mid + lo to 2^-24 relative), each [cout/32][ceil(cin/16)][64 lanes][8] in MFMA
- * fragment order (lane 32h + r, element j holds W[32t + r][(k + rot) % cin], k = 16kb +
- * (j&3) + 8(j>>2) + 4h; 0 past cin).  pn2_layer_split_bytes(cout, cin) bytes, 16-byte aligned.
- * Chains given wt_split for every layer (3 layers, grouped rows, hidden widths 32..128) run as
- * one register-resident kernel with fp32-accurate 6-product bf16 MFMA arithmetic; others (and
- * PN2_MLP_PATH=f32) use the fp32 MFMA kernels. */
-int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin);
-int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t rot, void *out,
-                              void *stream);
+ * W = hi + mid + lo to 2^-24 relative), each [cout/32][kblocks][64 lanes][8] in MFMA fragment
+ * order.  Kernel input channel k (block k/16) maps to W's input channel as follows:
+ *   xyz == 0 (hidden layers): k.   xyz > 0 (first layer, rows [xyz | features], D = cin-xyz):
+ *   block 0 holds the xyz channels (k < xyz), blocks >= 1 the features (k-16 < D); W's own
+ *   order is [xyz, features] if xyz_first (sample_and_group) else [features, xyz] (MSG).
+ * Lane 32h + r, element j of fragment (t, kb) holds W[32t + r][in(16kb + (j&3) + 8(j>>2) + 4h)]
+ * (0 for padding).  kblocks = pn2_layer_split_kblocks(cin, xyz); the image takes
+ * pn2_layer_split_bytes(cout, cin, xyz) bytes, 16-byte aligned.  Chains given wt_split for
+ * every layer (3 layers, grouped rows, hidden widths 32..128) run as one register-resident
+ * kernel with fp32-accurate 6-product bf16 MFMA arithmetic; others (and PN2_MLP_PATH=f32) use
+ * the fp32 MFMA kernels. */
+int64_t pn2_layer_split_kblocks(int64_t cin, int64_t xyz);
+int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin, int64_t xyz);
+int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t xyz,
+                              int xyz_first, void *out, void *stream);
 
 typedef struct pn2_sa_src {
     int mode; /* PN2_SRC_* */

@@ -58,6 +58,8 @@ struct ChainArgs {
     int vec_feat;
     float *out;
     int64_t ostride;
+    int lds_bn;    // byte offset of the staged BN scale/shift
+    int lds_ring;  // byte offset of the per-wave weight rings
 };
 
 struct Split {
@@ -82,14 +84,25 @@ __device__ __forceinline__ Split split8(const float (&x)[8]) {
 }
 
 #define PN2_MFMA16 __builtin_amdgcn_mfma_f32_32x32x16_bf16
-// acc += a * b with both operands split (6 bf16 products)
-__device__ __forceinline__ cfloatx16 mma6(const Split &a, const Split &b, cfloatx16 acc) {
-    acc = PN2_MFMA16(a.l, b.h, acc, 0, 0, 0);
-    acc = PN2_MFMA16(a.h, b.l, acc, 0, 0, 0);
-    acc = PN2_MFMA16(a.m, b.m, acc, 0, 0, 0);
-    acc = PN2_MFMA16(a.m, b.h, acc, 0, 0, 0);
-    acc = PN2_MFMA16(a.h, b.m, acc, 0, 0, 0);
-    acc = PN2_MFMA16(a.h, b.h, acc, 0, 0, 0);
+// acc += a * b with both operands split (6 bf16 products).  The weight operand's planes are
+// consumed in the order they are read from the ring (hi, mid, lo), so the first products can
+// start while the later planes are still in flight.
+__device__ __forceinline__ cfloatx16 mma6_wa(const Split &w, const Split &x, cfloatx16 acc) {
+    acc = PN2_MFMA16(w.h, x.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.h, x.m, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.h, x.l, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.m, x.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.m, x.m, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.l, x.h, acc, 0, 0, 0);
+    return acc;
+}
+__device__ __forceinline__ cfloatx16 mma6_wb(const Split &x, const Split &w, cfloatx16 acc) {
+    acc = PN2_MFMA16(x.h, w.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.m, w.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.l, w.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.h, w.m, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.m, w.m, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.h, w.l, acc, 0, 0, 0);
     return acc;
 }
 
@@ -104,13 +117,15 @@ __device__ __forceinline__ Split load_w(const ChainLayer &L, int t, int kb, int 
 }
 
 // BN + ReLU of a transposed hidden tile, split into the next layer's k-blocks 2t, 2t+1
-__device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const ChainLayer &L, int t,
-                                                int h, Split &lo, Split &hi) {
+// al/be: this layer's BN scale/shift staged in LDS
+__device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const float *al,
+                                                const float *be, int t, int h, Split &lo,
+                                                Split &hi) {
     cfloatx4 a4[4], b4[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-        a4[m] = *reinterpret_cast<const cfloatx4 *>(L.alpha + 32 * t + 8 * m + 4 * h);
-        b4[m] = *reinterpret_cast<const cfloatx4 *>(L.beta + 32 * t + 8 * m + 4 * h);
+        a4[m] = *reinterpret_cast<const cfloatx4 *>(al + 32 * t + 8 * m + 4 * h);
+        b4[m] = *reinterpret_cast<const cfloatx4 *>(be + 32 * t + 8 * m + 4 * h);
     }
     float y0[8], y1[8];
 #pragma unroll
@@ -122,9 +137,59 @@ __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const Chai
     hi = split8(y1);
 }
 
-template <int T0, int T1>
-__global__ __launch_bounds__(64 * kChainWaves) void sa_chain_kernel(const ChainArgs A) {
-    extern __shared__ __attribute__((aligned(16))) unsigned cpool[];
+
+// ---- per-wave weight ring (layers 1 and 2).  A step = one (tile, k-block) of a layer = its
+// three 1 KB plane fragments, copied HBM/L2 -> LDS by global_load_lds (lane-linear, no VGPRs)
+// R-1 steps ahead of use into this wave's own ring of R slots: no cross-wave barrier, and the
+// only vector-memory traffic in flight is the ring (BN parameters are staged in LDS), so a
+// counted s_waitcnt vmcnt retires exactly the step about to be read.
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr int kStepBytes = 3 * 1024;
+
+// frag: the step's plane-0 fragment (wave-uniform); loff = lane * 16 -- the uniform-base +
+// lane-offset form lets the copy use a scalar base address (no per-copy vector address math)
+__device__ __forceinline__ void ring_issue(const bf16x8 *frag, int64_t plane, char *slot,
+                                           unsigned loff) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char *>(frag + p * plane) + loff,
+                                         (lds_void *)(slot + p * 1024), 16, 0, 0);
+}
+
+__device__ __forceinline__ Split ring_read(const char *slot, int lane) {
+    const bf16x8 *q = reinterpret_cast<const bf16x8 *>(slot) + lane;
+    Split w;
+    w.h = q[0];
+    w.m = q[64];
+    w.l = q[128];
+    return w;
+}
+
+// Every consumed step has exactly NR-2 later steps in flight (issues past the end repeat the
+// last step into an already-consumed slot), so one constant count retires the step to read;
+// stores issued meanwhile only make the count conservative.
+template <int NR>
+__device__ __forceinline__ void ring_wait() {
+    if constexpr (NR == 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (NR == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// lanes l and l^32 exchange x (the two halves of a 32x32 tile column)
+__device__ __forceinline__ float swap_halves(float x) {
+    return __shfl_xor(x, 32);
+}
+
+// KB0M > 0: the layer-0 input (<= KB0M k-blocks) is gathered once into registers and layer 0 runs
+// tile by tile from the ring like layers 1 and 2; KB0M == 0: layer 0 streams its input blocks
+// (k-outer, every output tile accumulating) with ordinary loads and the ring starts at layer 1.
+template <int T0, int T1, int KB0M>
+__global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_eu(2))) void sa_chain_kernel(
+    const ChainArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char csm[];
+    constexpr int NR = (T0 * T1 >= 8) ? 4 : 3;  // ring slots
+    constexpr int KB1 = 2 * T0, KB2 = 2 * T1;
+    unsigned *cpool = reinterpret_cast<unsigned *>(csm);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int r = lane & 31, h = lane >> 5;
@@ -135,10 +200,47 @@ __global__ __launch_bounds__(64 * kChainWaves) void sa_chain_kernel(const ChainA
     const int coutL = 32 * L2.tiles;
     const int gpb = kChainRows / A.K;  // groups per workgroup (pool_mode 1)
 
-    if (A.pool_mode == 1) {
+    // stage BN scale/shift of the three layers: [al0|be0|al1|be1|al2|be2]
+    float *bn = reinterpret_cast<float *>(csm + A.lds_bn);
+    float *al0 = bn, *be0 = al0 + 32 * T0, *al1 = be0 + 32 * T0, *be1 = al1 + 32 * T1;
+    float *al2 = be1 + 32 * T1, *be2 = al2 + coutL;
+    for (int e = tid; e < 32 * T0; e += 64 * kChainWaves) { al0[e] = L0.alpha[e]; be0[e] = L0.beta[e]; }
+    for (int e = tid; e < 32 * T1; e += 64 * kChainWaves) { al1[e] = L1.alpha[e]; be1[e] = L1.beta[e]; }
+    for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
+    if (A.pool_mode == 1)
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
-        __syncthreads();
-    }
+    __syncthreads();
+    char *ring = csm + A.lds_ring + wave * (NR * kStepBytes);
+    const unsigned loff = (unsigned)lane * 16u;
+    // Ring steps in consumption order: layer 0 (resident input) block-major, then layers 1 and
+    // 2 tile-major.  Each consumed step issues the step NR-1 ahead; its source address comes
+    // from scalar arithmetic on the layer's base (compile-time inside the unrolled loops), and
+    // past the end the last step repeats into an already-consumed slot.
+    int nissued = 0, nread = 0;
+    auto issue_l = [&](const ChainLayer &L, int t, int kb) {
+        ring_issue(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64,
+                   ring + (nissued % NR) * kStepBytes, loff);
+        ++nissued;
+    };
+    auto issue2 = [&](int z) {  // layer-2 step z
+        z = min(z, L2.tiles * KB2 - 1);
+        issue_l(L2, z / KB2, z % KB2);
+    };
+    auto issue1 = [&](int y) {  // layer-1 step y
+        if (y < T1 * KB1) issue_l(L1, y / KB1, y % KB1);
+        else issue2(y - T1 * KB1);
+    };
+    const int n0 = T0 * L0.kb;
+    auto issue0 = [&](int x) {  // layer-0 step x (block-major)
+        if (x < n0) issue_l(L0, x % T0, x / T0);
+        else issue1(x - n0);
+    };
+    auto read_w = [&]() {
+        ring_wait<NR>();
+        const Split w = ring_read(ring + (nread % NR) * kStepBytes, lane);
+        ++nread;
+        return w;
+    };
 
     // ---- this lane's row: (group g, batch b, point n)
     const unsigned R = (unsigned)slab * 32u + (unsigned)r;
@@ -151,34 +253,69 @@ __global__ __launch_bounds__(64 * kChainWaves) void sa_chain_kernel(const ChainA
     const float *crow = s.ctr + (int64_t)g * A.C;
     const int D = A.D, C = A.C;
 
-    // 4 channels [c, c+4) of the row layout [feature | xyz - centroid | 0]
-    auto load_run = [&](int c, float *v) {
-        if (!valid) {
+    // Row layout: block 0 = [xyz - centroid | 0], blocks >= 1 = features (16 per block).  Lane
+    // (r, h) holds channels 16kb + (j&3) + 8(j>>2) + 4h of its row in element j.
+    auto load_x = [&](int kb, float (&x)[8]) {
+        if (kb == 0) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = 0.f;
-        } else if (A.vec_feat && c + 4 <= D) {
-            const cfloatx4 q = *reinterpret_cast<const cfloatx4 *>(frow + c);
+            for (int j = 0; j < 8; ++j) {
+                const int ch = (j & 3) + 8 * (j >> 2) + 4 * h;
+                x[j] = (valid && ch < C) ? __fsub_rn(prow[(int64_t)ch * s.pc], crow[ch]) : 0.f;
+            }
+            return;
+        }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = q[i];
-        } else {
+        for (int run = 0; run < 2; ++run) {
+            const int f = 16 * (kb - 1) + 8 * run + 4 * h;
+            if (A.vec_feat) {
+                cfloatx4 q = {0.f, 0.f, 0.f, 0.f};
+                if (valid && f < D) q = *reinterpret_cast<const cfloatx4 *>(frow + f);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int ch = c + i;
-                v[i] = ch < D ? frow[ch]
-                     : ch < D + C ? __fsub_rn(prow[(int64_t)(ch - D) * s.pc], crow[ch - D])
-                     : 0.f;
+                for (int i = 0; i < 4; ++i) x[4 * run + i] = q[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[4 * run + i] = (valid && f + i < D) ? frow[f + i] : 0.f;
             }
         }
     };
-    // lane (r, h) holds channels 16kb + (j&3) + 8(j>>2) + 4h of its row in element j
-    auto load_x = [&](int kb, float (&x)[8]) {
-        load_run(16 * kb + 4 * h, x);
-        load_run(16 * kb + 8 + 4 * h, x + 4);
-    };
 
-    // ---- layer 0: stream the gathered input, accumulate every output tile (transposed)
     Split X1[2 * T0];
-    {
+    if constexpr (KB0M > 0) {
+        // ---- layer 0 from registers: the whole input gathered once (raw fp32), then k-outer
+        // (each block split once, every output tile accumulating) with weights from the ring
+        float x[KB0M][8];
+#pragma unroll
+        for (int kb = 0; kb < KB0M; ++kb) {
+            if (kb < L0.kb) {
+                load_x(kb, x[kb]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[kb][j] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NR - 1; ++j) issue0(j);  // overlaps the gather's latency
+        cfloatx16 acc[T0];
+#pragma unroll
+        for (int t = 0; t < T0; ++t)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < KB0M; ++kb) {
+            if (kb < L0.kb) {
+                const Split xs = split8(x[kb]);
+#pragma unroll
+                for (int t = 0; t < T0; ++t) {
+                    const Split w = read_w();
+                    issue0(kb * T0 + t + NR - 1);
+                    acc[t] = mma6_wa(w, xs, acc[t]);
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < T0; ++t) hidden_epilogue(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+    } else {
+        // ---- layer 0 streamed: k-outer, every output tile accumulating (transposed)
         cfloatx16 acc[T0];
 #pragma unroll
         for (int t = 0; t < T0; ++t)
@@ -193,10 +330,13 @@ __global__ __launch_bounds__(64 * kChainWaves) void sa_chain_kernel(const ChainA
             if (kb + 1 < L0.kb) load_x(kb + 1, xn);
             const Split xs = split8(x);
 #pragma unroll
-            for (int t = 0; t < T0; ++t) acc[t] = mma6(load_w(L0, t, kb, lane), xs, acc[t]);
+            for (int t = 0; t < T0; ++t) acc[t] = mma6_wa(load_w(L0, t, kb, lane), xs, acc[t]);
         }
+        // layer 0's loads are all consumed: start the ring, then the epilogue hides its latency
 #pragma unroll
-        for (int t = 0; t < T0; ++t) hidden_epilogue(acc[t], L0, t, h, X1[2 * t], X1[2 * t + 1]);
+        for (int j = 0; j < NR - 1; ++j) issue1(j);
+#pragma unroll
+        for (int t = 0; t < T0; ++t) hidden_epilogue(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
     }
 
     // ---- layer 1: input in registers, one output tile at a time (transposed)
@@ -207,8 +347,12 @@ __global__ __launch_bounds__(64 * kChainWaves) void sa_chain_kernel(const ChainA
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < 2 * T0; ++kb) acc = mma6(load_w(L1, t, kb, lane), X1[kb], acc);
-        hidden_epilogue(acc, L1, t, h, X2[2 * t], X2[2 * t + 1]);
+        for (int kb = 0; kb < KB1; ++kb) {
+            const Split w = read_w();
+            issue1(t * KB1 + kb + NR - 1);
+            acc = mma6_wa(w, X1[kb], acc);
+        }
+        hidden_epilogue(acc, al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
     }
 
     // ---- layer 2: standard orientation, pooled over the neighbourhood
@@ -218,42 +362,53 @@ __global__ __launch_bounds__(64 * kChainWaves) void sa_chain_kernel(const ChainA
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < 2 * T1; ++kb) acc = mma6(X2[kb], load_w(L2, t, kb, lane), acc);
+        for (int kb = 0; kb < KB2; ++kb) {
+            const Split w = read_w();
+            issue2(t * KB2 + kb + NR - 1);
+            acc = mma6_wb(X2[kb], w, acc);
+        }
+        // max over rows of relu(fma(acc, al, be)) = relu(fma(extreme, al, be)) exactly: fma with
+        // a fixed al is monotone in acc (non-decreasing for al >= 0, else non-increasing) and
+        // so is relu -- only the row max (al >= 0) or min of the accumulator is needed.
+        // Register q of lane half h is row (q&3) + 8(q>>2) + 4h of the slab.
         const int col = 32 * t + r;
-        const float al = L2.alpha[col], be = L2.beta[col];
-        float v[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = chain_relu(__builtin_fmaf(acc[q], al, be));
-        // register q of lane half h is row (q&3) + 8(q>>2) + 4h of the slab
+        const float al = al2[col], be = be2[col];
+        const bool up = al >= 0.f;
+        auto fin = [&](float mx, float mn) { return chain_relu(__builtin_fmaf(up ? mx : mn, al, be)); };
         if (A.K == 8 || A.K == 16) {
-            constexpr int kParts = 4;
-            float m[kParts];
+            float mx[4], mn[4];
 #pragma unroll
-            for (int k = 0; k < kParts; ++k)
-                m[k] = fmaxf(fmaxf(v[4 * k], v[4 * k + 1]), fmaxf(v[4 * k + 2], v[4 * k + 3]));
-#pragma unroll
-            for (int k = 0; k < kParts; ++k) m[k] = fmaxf(m[k], __shfl_xor(m[k], 32));
-            // rows 8k..8k+7 of the slab are register group k (both halves)
+            for (int k = 0; k < 4; ++k) {  // rows 8k..8k+7 of the slab: registers 4k..4k+3, both halves
+                mx[k] = fmaxf(fmaxf(acc[4 * k], acc[4 * k + 1]), fmaxf(acc[4 * k + 2], acc[4 * k + 3]));
+                mn[k] = fminf(fminf(acc[4 * k], acc[4 * k + 1]), fminf(acc[4 * k + 2], acc[4 * k + 3]));
+                mx[k] = fmaxf(mx[k], swap_halves(mx[k]));
+                mn[k] = fminf(mn[k], swap_halves(mn[k]));
+            }
             if (h == 0) {
                 if (A.K == 8) {
 #pragma unroll
-                    for (int k = 0; k < kParts; ++k) {
+                    for (int k = 0; k < 4; ++k) {
                         const unsigned gg = (unsigned)slab * 4u + k;
-                        if (gg < G) A.out[(int64_t)gg * A.ostride + col] = m[k];
+                        if (gg < G) A.out[(int64_t)gg * A.ostride + col] = fin(mx[k], mn[k]);
                     }
                 } else {
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
                         const unsigned gg = (unsigned)slab * 2u + k;
-                        if (gg < G) A.out[(int64_t)gg * A.ostride + col] = fmaxf(m[2 * k], m[2 * k + 1]);
+                        if (gg < G)
+                            A.out[(int64_t)gg * A.ostride + col] =
+                                fin(fmaxf(mx[2 * k], mx[2 * k + 1]), fminf(mn[2 * k], mn[2 * k + 1]));
                     }
                 }
             }
         } else {
-            float m = 0.f;
+            float mx = acc[0], mn = acc[0];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) m = fmaxf(m, v[q]);
-            m = fmaxf(m, __shfl_xor(m, 32));
+            for (int q = 1; q < 16; ++q) {
+                mx = fmaxf(mx, acc[q]);
+                mn = fminf(mn, acc[q]);
+            }
+            const float m = fin(fmaxf(mx, swap_halves(mx)), fminf(mn, swap_halves(mn)));
             const unsigned gg = ((unsigned)slab * 32u) / (unsigned)A.K;
             if (h == 0 && (unsigned)slab * 32u < (unsigned)A.M) {
                 if (A.pool_mode == 0) A.out[(int64_t)gg * A.ostride + col] = m;
@@ -264,6 +419,7 @@ __global__ __launch_bounds__(64 * kChainWaves) void sa_chain_kernel(const ChainA
             }
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing (repeat) copies
     if (A.pool_mode == 1) {
         __syncthreads();
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) {
@@ -276,17 +432,34 @@ __global__ __launch_bounds__(64 * kChainWaves) void sa_chain_kernel(const ChainA
 
 // hidden-width signatures (output tiles of layers 0 and 1) compiled; the reference heads use
 // SSG [64,64,128] [128,128,256], MSG [32,32,64] [64,64,128] [64,96,128] [128,128,256]
-#define PN2_CHAIN_SIGS(X) X(1, 1) X(2, 2) X(2, 3) X(4, 4)
+// (T0, T1, KB0M): KB0M = 1 for xyz-only inputs (sa1 layers), 9 for 131/138-channel inputs
+// (SSG/pose sa2), 0 = streamed layer-0 input (any width)
+#define PN2_CHAIN_SIGS(X) \
+    X(1, 1, 1) X(2, 2, 1) X(2, 3, 1) X(4, 4, 9) X(1, 1, 0) X(2, 2, 0) X(2, 3, 0) X(4, 4, 0)
 
 }  // namespace pn2
 
 using namespace pn2;
 
 // ------------------------------------------------------------------ weight packing
-// plane p, tile t, block kb, lane l = 32h + r, element j:
-//   W[32t + r][(k + rot) % cin] with k = 16kb + (j&3) + 8(j>>2) + 4h  (0 for k >= cin)
+// Kernel input channel k of a layer (k-block kb = k / 16) -> input channel of W:
+//   xyz == 0 (hidden layers)  k (0 past cin)
+//   xyz  > 0 (first layer: rows [xyz | features], D = cin - xyz)
+//             block 0 holds xyz - centroid (k < xyz), blocks >= 1 the features (k - 16 < D);
+//             W's order is [xyz, features] when xyz_first (sample_and_group, :114), else
+//             [features, xyz] (PointNetSetAbstractionMsg, :209).
+// Fragment element: plane p, tile t, block kb, lane l = 32h + r, element j holds
+//   W[32t + r][in(16kb + (j&3) + 8(j>>2) + 4h)]  split into bf16 planes hi / mid / lo.
+__device__ __forceinline__ int split_in_channel(int k, int cin, int xyz, int xyz_first) {
+    if (xyz == 0) return k < cin ? k : -1;
+    const int D = cin - xyz;
+    if (k < 16) return k < xyz ? (xyz_first ? k : D + k) : -1;
+    const int f = k - 16;
+    return f < D ? (xyz_first ? xyz + f : f) : -1;
+}
+
 __global__ __launch_bounds__(256) void pack_split_kernel(const float *__restrict__ W, int cout,
-                                                          int cin, int kbs, int rot,
+                                                          int cin, int kbs, int xyz, int xyz_first,
                                                           __bf16 *__restrict__ out) {
     const int64_t per_plane = (int64_t)cout * kbs * 16;
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -296,8 +469,8 @@ __global__ __launch_bounds__(256) void pack_split_kernel(const float *__restrict
     const int64_t f = e >> 9;  // fragment = t * kbs + kb
     const int kb = (int)(f % kbs), t = (int)(f / kbs);
     const int r = l & 31, h = l >> 5;
-    const int k = 16 * kb + (j & 3) + 8 * (j >> 2) + 4 * h;
-    const float w = k < cin ? W[(int64_t)(32 * t + r) * cin + (k + rot) % cin] : 0.f;
+    const int ci = split_in_channel(16 * kb + (j & 3) + 8 * (j >> 2) + 4 * h, cin, xyz, xyz_first);
+    const float w = ci >= 0 ? W[(int64_t)(32 * t + r) * cin + ci] : 0.f;
     const __bf16 a = (__bf16)w;
     const float r1 = w - (float)a;
     const __bf16 m = (__bf16)r1;
@@ -307,22 +480,28 @@ __global__ __launch_bounds__(256) void pack_split_kernel(const float *__restrict
     out[2 * per_plane + e] = lo;
 }
 
-extern "C" int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin) {
-    if (cout < 32 || cout % 32 != 0 || cin < 1) return -1;
-    return 3 * cout * ((cin + 15) / 16) * 16 * 2;
+extern "C" int64_t pn2_layer_split_kblocks(int64_t cin, int64_t xyz) {
+    if (cin < 1 || xyz < 0 || xyz > 16 || xyz > cin) return -1;
+    return xyz > 0 ? 1 + (cin - xyz + 15) / 16 : (cin + 15) / 16;
 }
 
-extern "C" int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t rot,
-                                         void *out, void *stream) {
+extern "C" int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin, int64_t xyz) {
+    const int64_t kbs = pn2_layer_split_kblocks(cin, xyz);
+    if (cout < 32 || cout % 32 != 0 || kbs < 0) return -1;
+    return 3 * cout * kbs * 16 * 2;
+}
+
+extern "C" int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t xyz,
+                                         int xyz_first, void *out, void *stream) {
     PN2_REQUIRE(W && out, "pn2_pack_layer_split_bf16: null pointer");
-    PN2_REQUIRE(cout >= 32 && cout % 32 == 0 && cin >= 1 && rot >= 0 && rot < cin,
-                "pn2_pack_layer_split_bf16: bad shape cout=%lld cin=%lld rot=%lld", (long long)cout,
-                (long long)cin, (long long)rot);
+    const int64_t kbs = pn2_layer_split_kblocks(cin, xyz);
+    PN2_REQUIRE(cout >= 32 && cout % 32 == 0 && kbs > 0,
+                "pn2_pack_layer_split_bf16: bad shape cout=%lld cin=%lld xyz=%lld", (long long)cout,
+                (long long)cin, (long long)xyz);
     PN2_REQUIRE(((uintptr_t)out & 15) == 0, "pn2_pack_layer_split_bf16: output not 16-byte aligned");
-    const int kbs = (int)((cin + 15) / 16);
     const int64_t per_plane = cout * kbs * 16;
     hipLaunchKernelGGL(pack_split_kernel, dim3((unsigned)((per_plane + 255) / 256)), dim3(256), 0,
-                       as_stream(stream), W, (int)cout, (int)cin, kbs, (int)rot,
+                       as_stream(stream), W, (int)cout, (int)cin, (int)kbs, (int)xyz, xyz_first ? 1 : 0,
                        reinterpret_cast<__bf16 *>(out));
     PN2_LAUNCH_CHECK("pack_split_kernel");
     return PN2_OK;
@@ -331,19 +510,22 @@ extern "C" int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t c
 // ------------------------------------------------------------------ host: dispatch
 namespace pn2 {
 
-template <int T0, int T1>
+template <int T0, int T1, int KB0M>
 static int launch_chain_sig(const ChainArgs &A, unsigned grid, size_t lds, hipStream_t st) {
-    hipLaunchKernelGGL((sa_chain_kernel<T0, T1>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
+    hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
     PN2_LAUNCH_CHECK("sa_chain_kernel");
     return PN2_OK;
 }
 
-static bool chain_sig_compiled(int T0, int T1) {
-#define PN2_CHAIN_HAS(a, b) \
-    if (T0 == a && T1 == b) return true;
+// the compiled KB0M for this chain: the smallest resident bound >= kb0, else 0 (streamed);
+// -1 when (T0, T1) has no instance
+static int chain_kb0m(int T0, int T1, int kb0) {
+    int best = -1;
+#define PN2_CHAIN_HAS(a, b, c) \
+    if (T0 == a && T1 == b && (c == 0 ? best < 0 : (kb0 <= c && (best <= 0 || c < best)))) best = c;
     PN2_CHAIN_SIGS(PN2_CHAIN_HAS)
 #undef PN2_CHAIN_HAS
-    return false;
+    return best;
 }
 
 // 1: launched, 0: this chain is not eligible (caller uses the fp32 kernels), <0: error
@@ -357,9 +539,14 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     for (int l = 0; l < 3; ++l)
         if (!layers[l].wt_split || ((uintptr_t)layers[l].wt_split & 15)) return 0;
     const int T0 = (int)(layers[0].cout / 32), T1 = (int)(layers[1].cout / 32);
-    if (!chain_sig_compiled(T0, T1)) return 0;
-    if (!(K == 8 || K == 16 || K % 32 == 0)) return 0;
-
+    // k-blocks per layer (the first layer's rows are [xyz | features], see split_in_channel)
+    int kbs[3];
+    kbs[0] = (int)pn2_layer_split_kblocks(layers[0].cin, s.C);
+    kbs[1] = (int)((layers[1].cin + 15) / 16);
+    kbs[2] = (int)((layers[2].cin + 15) / 16);
+    if (kbs[0] < 1) return 0;
+    const int KB0M = chain_kb0m(T0, T1, kbs[0]);
+    if (KB0M < 0) return 0;
     ChainArgs A;
     memset(&A, 0, sizeof(A));
     A.src = s;
@@ -367,7 +554,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         A.L[l].w = reinterpret_cast<const bf16x8 *>(layers[l].wt_split);
         A.L[l].alpha = layers[l].alpha;
         A.L[l].beta = layers[l].beta;
-        A.L[l].kb = (int)((layers[l].cin + 15) / 16);
+        A.L[l].kb = kbs[l];
         A.L[l].tiles = (int)(layers[l].cout / 32);
     }
     A.M = (int)M;
@@ -389,7 +576,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     } else {
         A.pool_mode = 2;
     }
-    if (lds > 64 * 1024) A.pool_mode = 2, lds = 0;
+    if (lds > 32 * 1024) A.pool_mode = 2, lds = 0;
     if (A.pool_mode == 2) {
         const int64_t G = M / K;
         hipError_t e = (ostride == coutL)
@@ -398,9 +585,15 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         if (e != hipSuccess) return set_error(PN2_EHIP, "sa_chain: memset: %s", hipGetErrorString(e));
     }
     const unsigned grid = (unsigned)((M + kChainRows - 1) / kChainRows);
+    // LDS: [pool][BN scale/shift][per-wave rings]
+    A.lds_bn = (int)((lds + 15) / 16 * 16);
+    const size_t bn_bytes = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + coutL);
+    A.lds_ring = (int)((A.lds_bn + bn_bytes + 15) / 16 * 16);
+    const int ring_slots = (T0 * T1 >= 8) ? 4 : 3;  // = NR of sa_chain_kernel
+    lds = (size_t)A.lds_ring + (size_t)kChainWaves * ring_slots * kStepBytes;
     int rc = PN2_EUNSUPPORTED;
-#define PN2_CHAIN_GO(a, b) \
-    if (T0 == a && T1 == b) rc = launch_chain_sig<a, b>(A, grid, lds, st);
+#define PN2_CHAIN_GO(a, b, c) \
+    if (T0 == a && T1 == b && KB0M == c) rc = launch_chain_sig<a, b, c>(A, grid, lds, st);
     PN2_CHAIN_SIGS(PN2_CHAIN_GO)
 #undef PN2_CHAIN_GO
     return rc == PN2_OK ? 1 : rc;

@@ -63,9 +63,10 @@ SIGNATURES = {
                              _vp, _i64, _vp, _i64, _int, _vp, _vp]),
     "pn2_layer_cin_pad": (_i64, [_i64]),
     "pn2_pack_layer_f32": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _dbl, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
-    "pn2_layer_split_bytes": (_i64, [_i64, _i64]),
+    "pn2_layer_split_kblocks": (_i64, [_i64, _i64]),
+    "pn2_layer_split_bytes": (_i64, [_i64, _i64, _i64]),
     "pn2_sa_mlp_last_path": (_int, []),
-    "pn2_pack_layer_split_bf16": (_int, [_vp, _i64, _i64, _i64, _vp, _vp]),
+    "pn2_pack_layer_split_bf16": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp]),
     "pn2_sa_mlp_workspace_bytes": (_i64, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int]),
     "pn2_sa_mlp_max_f32": (_int, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int, _int, _vp,
                                   _i64, _vp, _i64, _vp]),

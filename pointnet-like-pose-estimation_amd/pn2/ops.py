@@ -269,26 +269,29 @@ def _(weight, bias, gamma, beta, mean, var, eps, rot):
 
 
 @torch.library.custom_op("pn2::pack_layer_split", mutates_args=())
-def pack_layer_split(weight: Tensor, rot: int) -> Tensor:
+def pack_layer_split(weight: Tensor, xyz: int, xyz_first: bool) -> Tensor:
     """Conv2d 1x1 weight [cout,cin,1,1] -> the split-bf16 image of pn2_pack_layer_split_bf16
-    (three bf16 planes hi/mid/lo in MFMA fragment order, same `rot` as pack_layer), flat
-    bfloat16.  Used by the register-resident chain kernel (sa_chain.hip)."""
+    (three bf16 planes hi/mid/lo in MFMA fragment order), flat bfloat16.  xyz: the xyz channels
+    of a first layer (its rows are [xyz | features] in the chain kernel; 0 for hidden layers),
+    xyz_first: W's own order is [xyz, features] (SSG) rather than [features, xyz] (MSG)."""
     _dev(weight, "pn2::pack_layer_split")
     cout, cin = weight.shape[0], weight.shape[1]
     w = weight.reshape(cout, cin).contiguous()
-    nbytes = int(_L.pn2_layer_split_bytes(cout, cin))
+    nbytes = int(_L.pn2_layer_split_bytes(cout, cin, xyz))
     if nbytes < 0:
-        raise ValueError("pn2::pack_layer_split: cout=%d must be a positive multiple of 32" % cout)
+        raise ValueError("pn2::pack_layer_split: bad shape cout=%d cin=%d xyz=%d" % (cout, cin, xyz))
     out = torch.empty(nbytes // 2, dtype=torch.bfloat16, device=weight.device)
     _run("pn2_pack_layer_split_bf16", _L.pn2_pack_layer_split_bf16,
-         (w.data_ptr(), cout, cin, int(rot), out.data_ptr(), _stream(weight)), weight.device)
+         (w.data_ptr(), cout, cin, int(xyz), 1 if xyz_first else 0, out.data_ptr(),
+          _stream(weight)), weight.device)
     return out
 
 
 @pack_layer_split.register_fake
-def _(weight, rot):
+def _(weight, xyz, xyz_first):
     cout, cin = weight.shape[0], weight.shape[1]
-    return weight.new_empty(3 * cout * ((cin + 15) // 16) * 16, dtype=torch.bfloat16)
+    kbs = 1 + (cin - xyz + 15) // 16 if xyz else (cin + 15) // 16
+    return weight.new_empty(3 * cout * kbs * 16, dtype=torch.bfloat16)
 
 
 # ------------------------------------------------------------------------------ sa_mlp_max_

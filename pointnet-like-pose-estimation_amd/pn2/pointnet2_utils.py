@@ -53,14 +53,17 @@ def _needs_autograd(module, *tensors):
         t is not None and t.requires_grad for t in tensors)
 
 
-def _pack_chain(convs, bns, cache, rot0):
-    """Fold each Conv2d-1x1 + eval BatchNorm2d into (W^T, alpha, beta); cached until any
-    parameter/buffer changes (data_ptr or in-place version).  rot0: xyz channels leading the
-    first layer's input in the reference's order (the kernels put them behind the features)."""
+def _pack_chain(convs, bns, cache, rot0, xyz=0, xyz_first=True):
+    """Fold each Conv2d-1x1 + eval BatchNorm2d into (W^T, alpha, beta) for the fp32 kernels and
+    the split-bf16 image for the chain kernel; cached until any parameter/buffer changes
+    (data_ptr or in-place version).  rot0: xyz channels leading the first layer's input in the
+    reference's order (the fp32 kernels put them behind the features); xyz / xyz_first: the
+    first layer's xyz channel count and order for the chain kernel (rows [xyz | features])."""
     tensors = []
     for conv, bn in zip(convs, bns):
         tensors += [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
-    key = (rot0,) + tuple((None if t is None else (t.data_ptr(), t._version)) for t in tensors)
+    key = (rot0, xyz, xyz_first) + tuple((None if t is None else (t.data_ptr(), t._version))
+                                         for t in tensors)
     if cache.get("key") != key:
         wts, als, bes, cins, splits = [], [], [], [], []
         with torch.no_grad():
@@ -72,7 +75,8 @@ def _pack_chain(convs, bns, cache, rot0):
                 als.append(al)
                 bes.append(be)
                 cins.append(conv.weight.shape[1])
-                splits.append(ops.pack_layer_split(conv.weight, rot))
+                splits.append(ops.pack_layer_split(conv.weight, xyz if li == 0 else 0,
+                                                   xyz_first))
         cache["key"] = key
         cache["layers"] = (wts, als, bes, cins, splits)
     return cache["layers"]
@@ -174,7 +178,9 @@ class PointNetSetAbstraction(nn.Module):
         B, N, C = pts.shape
         # reference row order is [xyz, feature] (:114, :139); kernels use [feature, xyz]
         rot0 = C if feat is not None else 0
-        wts, als, bes, cins, splits = _pack_chain(self.mlp_convs, self.mlp_bns, self._pack_cache, rot0)
+        xyz = 0 if self.group_all else C  # the chain kernel serves the grouped layers
+        wts, als, bes, cins, splits = _pack_chain(self.mlp_convs, self.mlp_bns, self._pack_cache,
+                                                  rot0, xyz, True)
         cout = wts[-1].shape[1]
         dev = pts.device
         if self.group_all:
@@ -239,7 +245,8 @@ class PointNetSetAbstractionMsg(nn.Module):
         S = self.point_number
         dev = pts.device
         # MSG row order is already [feature, xyz] (:209): no rotation
-        chains = [_pack_chain(self.conv_blocks[i], self.bn_blocks[i], self._pack_cache[i], 0)
+        chains = [_pack_chain(self.conv_blocks[i], self.bn_blocks[i], self._pack_cache[i], 0, C,
+                              False)
                   for i in range(len(self.radius_list))]
         total = sum(ch[0][-1].shape[1] for ch in chains)
         with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
