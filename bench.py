@@ -6,12 +6,14 @@ of N=1024 points per GPU, on the MI355X-native SA path.
 
 One step = one forward of the head over every rank's batch shard (weak scaling: B clouds per
 GPU, global batch = B*N) followed by the RCCL all_gather of the logits -- the only exchange the
-data-parallel path has.  The forward runs op by op (--graph replays it as a HIP graph via
-pn2.graphs.GraphedForward: same kernels and CPU-RNG draws; measured slower on MI355X, see
-DESIGN.md).  Inputs are resident in HBM before the timed region, which carries no
-instrumentation.  Rank 0 prints one JSON line (contract in the task statement) with:
-  value         clouds/s of the timed region; with --graph, eager_value is the same K steps op
-                by op.
+data-parallel path has.  Single-head configs run the K steps through pn2.pipeline (the FPS
+chain of step i+1 on a few dedicated CUs while step i's ball queries, MLPs and head run on the
+others; every step computes exactly the eager forward, with the same CPU-RNG draws);
+--no-pipeline runs them one after the other, --graph replays each as a HIP graph.  Inputs are
+resident in HBM before the timed region, which carries no instrumentation.  Rank 0 prints one
+JSON line (contract in the task statement) with:
+  value         clouds/s of the timed region; eager_value is the same K steps run one after
+                the other, op by op.
   roofline      dominant kernel = pn2_sa_mlp_max_f32 (the fused gather+MLP+max, fp32 MFMA):
                 achieved = algorithmic FLOPs (2*M*sum(cin*cout) per launch, cin unpadded) /
                 launch duration timed with HIP events on the launch stream, over a further
@@ -61,6 +63,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline sample")
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the forward as a HIP graph")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="plain eager steps (default for single-head configs: pn2.pipeline)")
+    ap.add_argument("--geometry-cus", type=int, default=32, help="CUs reserved for the FPS chain")
     return ap.parse_args()
 
 
@@ -171,16 +176,35 @@ def main():
     x, mean = make_inputs(a.config, hi - lo, lo, dev, rank)
     torch.manual_seed(1234)  # identical CPU RNG stream on every rank (FPS start draws)
 
+    # single-head configs run software-pipelined (pn2.pipeline: the FPS chain of step i+1 on
+    # its own CUs while step i's MLPs run); same kernels, results and RNG draws as eager steps
+    pipelined = len(eager_models) == 1 and not a.graph and not a.no_pipeline
+    pf = None
+    if pipelined:
+        from pn2.pipeline import PipelinedForward
+        pf = PipelinedForward(eager_models[0], geometry_cus=a.geometry_cus)
+
+    def run_pipelined(k):
+        with shard.batch_shard(gB, lo):
+            pf.run([x] * k, None if mean is None or not names[0].startswith("translation")
+                   else [(mean,)] * k,
+                   post=lambda i, o: shard.all_gather_rows(o[0] if isinstance(o, tuple) else o))
+
     for _ in range(max(a.warmup, 2) if a.graph else a.warmup):  # graph: 1st call captures
         step(names, models, x, mean, gB, lo)
+    if pipelined:
+        run_pipelined(max(a.warmup, 2))
     torch.cuda.synchronize()
 
-    def timed(k, timer, models=models):
+    def timed(k, timer, models=models, pipe=False):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if timer:
+        if pipe:
+            kt = None
+            run_pipelined(k)
+        elif timer:
             with ops.kernel_timer() as kt:
                 for _ in range(k):
                     step(names, models, x, mean, gB, lo)
@@ -201,12 +225,12 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    el, _ = timed(a.steps, False)
+    el, _ = timed(a.steps, False, pipe=pipelined)
     el = max_over_ranks(el)
     ms = el / a.steps * 1e3
     value = gB * a.steps / el
     eager_value = value
-    if a.graph:
+    if a.graph or pipelined:
         el_e, _ = timed(a.steps, False, eager_models)
         eager_value = gB * a.steps / max_over_ranks(el_e)
     kt = None
@@ -242,7 +266,9 @@ def main():
             "config": {"workload": desc, "global_batch": gB, "points": N, "heads": names,
                        "parallelism": "dp%d" % world},
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
-            "launch": "hip_graph" if a.graph else "eager", "eager_value": round(eager_value, 2),
+            "launch": ("hip_graph" if a.graph else
+                       "pipelined(fps on %d CUs)" % a.geometry_cus if pipelined else "eager"),
+            "eager_value": round(eager_value, 2),
         }
         print(json.dumps(line))
     if world > 1:

@@ -168,6 +168,12 @@ int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers, int n
 
 /* Which kernel family served this thread's last successful pn2_sa_mlp_max_f32 call:
  * PN2_PATH_F32 (fp32 MFMA kernels) or PN2_PATH_SPLIT_BF16 (register-resident chain). */
+/* ---- runtime: CU-partitioned streams (pipelined serving, pn2/pipeline.py) ---- */
+int pn2_device_cu_count(int device, int *count);
+/* A stream whose kernels run only on the CUs set in mask (bit i of word i/32 = CU i). */
+int pn2_stream_create_cu_masked(int device, const uint32_t *mask, int mask_words, void **stream);
+int pn2_stream_destroy(void *stream);
+
 #define PN2_PATH_F32 1
 #define PN2_PATH_SPLIT_BF16 2
 int pn2_sa_mlp_last_path(void);

@@ -165,15 +165,21 @@ __device__ __forceinline__ Split ring_read(const char *slot, int lane) {
     return w;
 }
 
-// Every consumed step has exactly NR-2 later steps in flight (issues past the end repeat the
-// last step into an already-consumed slot), so one constant count retires the step to read;
-// stores issued meanwhile only make the count conservative.
+// Step j refills the slot of step j-1 before waiting for its own copies, so NR-1 later steps
+// are in flight at every wait (issues past the end repeat the last step into an
+// already-consumed slot): one constant count retires step j; stores issued meanwhile only
+// make the count conservative.
 template <int NR>
 __device__ __forceinline__ void ring_wait() {
-    if constexpr (NR == 4) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if constexpr (NR == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    if constexpr (NR == 4) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if constexpr (NR == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+
+// Before a slot is refilled, the previous step's fragment reads from it must have returned.
+// The compiler does not see that global_load_lds (addressed through M0) writes that slot, so
+// the memory clobber also keeps those reads from being scheduled after the refill.
+__device__ __forceinline__ void ring_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // lanes l and l^32 exchange x (the two halves of a 32x32 tile column)
 __device__ __forceinline__ float swap_halves(float x) {
@@ -213,9 +219,10 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     char *ring = csm + A.lds_ring + wave * (NR * kStepBytes);
     const unsigned loff = (unsigned)lane * 16u;
     // Ring steps in consumption order: layer 0 (resident input) block-major, then layers 1 and
-    // 2 tile-major.  Each consumed step issues the step NR-1 ahead; its source address comes
-    // from scalar arithmetic on the layer's base (compile-time inside the unrolled loops), and
-    // past the end the last step repeats into an already-consumed slot.
+    // 2 tile-major.  Step j first refills the previous step's slot with step j+NR-1 (after
+    // ring_fence), then waits for and reads its own; source addresses come from scalar
+    // arithmetic on the layer's base (compile-time inside the unrolled loops), and past the end
+    // the last step repeats into an already-consumed slot.
     int nissued = 0, nread = 0;
     auto issue_l = [&](const ChainLayer &L, int t, int kb) {
         ring_issue(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64,
@@ -306,9 +313,9 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
                 const Split xs = split8(x[kb]);
 #pragma unroll
                 for (int t = 0; t < T0; ++t) {
-                    const Split w = read_w();
+                    ring_fence();
                     issue0(kb * T0 + t + NR - 1);
-                    acc[t] = mma6_wa(w, xs, acc[t]);
+                    acc[t] = mma6_wa(read_w(), xs, acc[t]);
                 }
             }
         }
@@ -348,9 +355,9 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
         for (int kb = 0; kb < KB1; ++kb) {
-            const Split w = read_w();
+            ring_fence();
             issue1(t * KB1 + kb + NR - 1);
-            acc = mma6_wa(w, X1[kb], acc);
+            acc = mma6_wa(read_w(), X1[kb], acc);
         }
         hidden_epilogue(acc, al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
     }
@@ -363,9 +370,9 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
         for (int kb = 0; kb < KB2; ++kb) {
-            const Split w = read_w();
+            ring_fence();
             issue2(t * KB2 + kb + NR - 1);
-            acc = mma6_wb(X2[kb], w, acc);
+            acc = mma6_wb(X2[kb], read_w(), acc);
         }
         // max over rows of relu(fma(acc, al, be)) = relu(fma(extreme, al, be)) exactly: fma with
         // a fixed al is monotone in acc (non-decreasing for al >= 0, else non-increasing) and

@@ -66,6 +66,9 @@ SIGNATURES = {
     "pn2_layer_split_kblocks": (_i64, [_i64, _i64]),
     "pn2_layer_split_bytes": (_i64, [_i64, _i64, _i64]),
     "pn2_sa_mlp_last_path": (_int, []),
+    "pn2_device_cu_count": (_int, [_int, ctypes.POINTER(_int)]),
+    "pn2_stream_create_cu_masked": (_int, [_int, ctypes.POINTER(ctypes.c_uint32), _int, ctypes.POINTER(_vp)]),
+    "pn2_stream_destroy": (_int, [_vp]),
     "pn2_pack_layer_split_bf16": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp]),
     "pn2_sa_mlp_workspace_bytes": (_i64, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int]),
     "pn2_sa_mlp_max_f32": (_int, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int, _int, _vp,

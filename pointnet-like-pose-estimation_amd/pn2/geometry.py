@@ -18,7 +18,9 @@ does not recycle them early.
 Opt-in with ``PN2_GEOMETRY_STREAM=1``; by default (and inside graph capture) everything stays
 on the caller's stream.
 """
+import contextlib
 import os
+import threading
 import weakref
 
 import torch
@@ -100,3 +102,34 @@ class Span:
             self.main.wait_event(ev)
             for t in used:
                 t.record_stream(self.main)
+
+
+# ----------------------------------------------------------------------------- provided FPS
+# pn2.pipeline runs a batch's FPS chain ahead of its forward; the SA modules then take the
+# precomputed (centroids, packed centroids, packed points) instead of drawing and sampling.
+_tls = threading.local()
+
+
+@contextlib.contextmanager
+def provide(entries):
+    """entries: {id(module): (input data_ptr, new_points, ctr_packed, pts_packed)}."""
+    prev = getattr(_tls, "entries", None)
+    _tls.entries = entries
+    try:
+        yield
+    finally:
+        _tls.entries = prev
+
+
+def take(module, pts):
+    """The provided FPS results for `module` called on `pts`, or None when nothing is provided.
+    A provided entry whose recorded input differs from `pts` is an error (the precomputed
+    sampling -- and the RNG draws behind it -- would not match this call)."""
+    entries = getattr(_tls, "entries", None)
+    if not entries or id(module) not in entries:
+        return None
+    ptr, newp, cpk, ppk = entries.pop(id(module))
+    if ptr != pts.data_ptr():
+        raise RuntimeError("pn2.pipeline: the SA module was called on a different point tensor "
+                           "than the one its FPS was precomputed for")
+    return newp, cpk, ppk

@@ -2,7 +2,9 @@
 
 Each op takes/returns torch tensors, checks shapes in Python (raising the exception the
 reference raises for the same misuse), and calls the HIP entry point asynchronously on torch's
-current stream.  Device tensors only: there is no CPU implementation and no fallback -- a CPU
+current stream.  ``<op>_direct`` is the same function without the torch.library dispatcher
+(the SA modules' eager path calls it: the dispatcher costs more host time per call than the
+kernels it launches take on the GPU at these sizes).  Device tensors only: there is no CPU implementation and no fallback -- a CPU
 tensor or a missing library is an error.
 
 Ops (reference code each replaces, in /root/reference/model/pointnet2_utils.py):
@@ -96,8 +98,7 @@ def cin_pad(cin: int) -> int:
 
 
 # ------------------------------------------------------------------------------ fps
-@torch.library.custom_op("pn2::fps", mutates_args=())
-def fps(points: Tensor, npoint: int, start: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+def fps_direct(points: Tensor, npoint: int, start: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """points [B,N,C] float32 (any strides), start [B] int64 -> (fps_idx [B,S] int64,
     new_points [B,S,C], packed centroids [B,S,cp], packed points [B,N,cp])."""
     _dev(points, "pn2::fps")
@@ -116,6 +117,9 @@ def fps(points: Tensor, npoint: int, start: Tensor) -> Tuple[Tensor, Tensor, Ten
     return idx, newp, cpk, ppk
 
 
+fps = torch.library.custom_op("pn2::fps", fps_direct, mutates_args=())
+
+
 @fps.register_fake
 def _(points, npoint, start):
     B, N, C = points.shape
@@ -125,8 +129,7 @@ def _(points, npoint, start):
 
 
 # ------------------------------------------------------------------------------ pack_points
-@torch.library.custom_op("pn2::pack_points", mutates_args=())
-def pack_points(points: Tensor) -> Tensor:
+def pack_points_direct(points: Tensor) -> Tensor:
     """[B,N,C] (any strides) -> [B,N,cp] records (coords, ssq in the reference's order, pad)."""
     _dev(points, "pn2::pack_points")
     B, N, C = points.shape
@@ -137,6 +140,9 @@ def pack_points(points: Tensor) -> Tensor:
     return out
 
 
+pack_points = torch.library.custom_op("pn2::pack_points", pack_points_direct, mutates_args=())
+
+
 @pack_points.register_fake
 def _(points):
     B, N, C = points.shape
@@ -144,8 +150,7 @@ def _(points):
 
 
 # ------------------------------------------------------------------------------ ball query
-@torch.library.custom_op("pn2::ball_query", mutates_args=())
-def ball_query(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, nsample: int) -> Tensor:
+def ball_query_direct(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, nsample: int) -> Tensor:
     """Packed points [B,N,cp] and centroids [B,S,cp] -> group_idx [B,S,nsample] int64."""
     _dev(pts_packed, "pn2::ball_query")
     B, N, _ = pts_packed.shape
@@ -162,14 +167,16 @@ def ball_query(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, ns
     return out
 
 
+ball_query = torch.library.custom_op("pn2::ball_query", ball_query_direct, mutates_args=())
+
+
 @ball_query.register_fake
 def _(pts_packed, ctr_packed, C, radius, nsample):
     return pts_packed.new_empty(pts_packed.shape[0], ctr_packed.shape[1], nsample, dtype=torch.int64)
 
 
 # ------------------------------------------------------------------------------ square_distance
-@torch.library.custom_op("pn2::square_distance", mutates_args=())
-def square_distance(src_packed: Tensor, dst_packed: Tensor, C: int) -> Tensor:
+def square_distance_direct(src_packed: Tensor, dst_packed: Tensor, C: int) -> Tensor:
     _dev(src_packed, "pn2::square_distance")
     B, S, _ = src_packed.shape
     N = dst_packed.shape[1]
@@ -180,14 +187,16 @@ def square_distance(src_packed: Tensor, dst_packed: Tensor, C: int) -> Tensor:
     return out
 
 
+square_distance = torch.library.custom_op("pn2::square_distance", square_distance_direct, mutates_args=())
+
+
 @square_distance.register_fake
 def _(src_packed, dst_packed, C):
     return src_packed.new_empty(src_packed.shape[0], src_packed.shape[1], dst_packed.shape[1])
 
 
 # ------------------------------------------------------------------------------ index_points
-@torch.library.custom_op("pn2::index_points", mutates_args=())
-def index_points(points: Tensor, idx: Tensor) -> Tensor:
+def index_points_direct(points: Tensor, idx: Tensor) -> Tensor:
     """points [B,N,C] (any strides), idx [B,M] int64 -> [B,M,C] contiguous."""
     _dev(points, "pn2::index_points")
     B, N, C = points.shape
@@ -201,14 +210,16 @@ def index_points(points: Tensor, idx: Tensor) -> Tensor:
     return out
 
 
+index_points = torch.library.custom_op("pn2::index_points", index_points_direct, mutates_args=())
+
+
 @index_points.register_fake
 def _(points, idx):
     return points.new_empty(points.shape[0], idx.shape[1], points.shape[2])
 
 
 # ------------------------------------------------------------------------------ group
-@torch.library.custom_op("pn2::group", mutates_args=())
-def group(points: Tensor, feature: Optional[Tensor], centers: Tensor, idx: Tensor,
+def group_direct(points: Tensor, feature: Optional[Tensor], centers: Tensor, idx: Tensor,
           feature_first: bool) -> Tensor:
     """[B,S,K,C+D]: [xyz(idx) - centre, feature(idx)] (or feature first, the MSG order)."""
     _dev(points, "pn2::group")
@@ -230,6 +241,9 @@ def group(points: Tensor, feature: Optional[Tensor], centers: Tensor, idx: Tenso
     return out
 
 
+group = torch.library.custom_op("pn2::group", group_direct, mutates_args=())
+
+
 @group.register_fake
 def _(points, feature, centers, idx, feature_first):
     D = 0 if feature is None else feature.shape[2]
@@ -237,8 +251,7 @@ def _(points, feature, centers, idx, feature_first):
 
 
 # ------------------------------------------------------------------------------ pack_layer
-@torch.library.custom_op("pn2::pack_layer", mutates_args=())
-def pack_layer(weight: Tensor, bias: Optional[Tensor], gamma: Optional[Tensor],
+def pack_layer_direct(weight: Tensor, bias: Optional[Tensor], gamma: Optional[Tensor],
                beta: Optional[Tensor], mean: Optional[Tensor], var: Optional[Tensor],
                eps: float, rot: int) -> Tuple[Tensor, Tensor, Tensor]:
     """Conv2d 1x1 weight [cout,cin,1,1] (+ bias) and eval BatchNorm2d stats -> (W^T pair-packed
@@ -261,6 +274,9 @@ def pack_layer(weight: Tensor, bias: Optional[Tensor], gamma: Optional[Tensor],
     return wt, al, be
 
 
+pack_layer = torch.library.custom_op("pn2::pack_layer", pack_layer_direct, mutates_args=())
+
+
 @pack_layer.register_fake
 def _(weight, bias, gamma, beta, mean, var, eps, rot):
     cout, cin = weight.shape[0], weight.shape[1]
@@ -268,8 +284,7 @@ def _(weight, bias, gamma, beta, mean, var, eps, rot):
     return e(cin_pad(cin) // 2, cout, 2), e(cout), e(cout)
 
 
-@torch.library.custom_op("pn2::pack_layer_split", mutates_args=())
-def pack_layer_split(weight: Tensor, xyz: int, xyz_first: bool) -> Tensor:
+def pack_layer_split_direct(weight: Tensor, xyz: int, xyz_first: bool) -> Tensor:
     """Conv2d 1x1 weight [cout,cin,1,1] -> the split-bf16 image of pn2_pack_layer_split_bf16
     (three bf16 planes hi/mid/lo in MFMA fragment order), flat bfloat16.  xyz: the xyz channels
     of a first layer (its rows are [xyz | features] in the chain kernel; 0 for hidden layers),
@@ -285,6 +300,9 @@ def pack_layer_split(weight: Tensor, xyz: int, xyz_first: bool) -> Tensor:
          (w.data_ptr(), cout, cin, int(xyz), 1 if xyz_first else 0, out.data_ptr(),
           _stream(weight)), weight.device)
     return out
+
+
+pack_layer_split = torch.library.custom_op("pn2::pack_layer_split", pack_layer_split_direct, mutates_args=())
 
 
 @pack_layer_split.register_fake
@@ -317,8 +335,7 @@ def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K):
     return s
 
 
-@torch.library.custom_op("pn2::sa_mlp_max_", mutates_args=("out",))
-def sa_mlp_max_(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor],
+def sa_mlp_max_direct(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor],
                 centers: Optional[Tensor], idx: Optional[Tensor], wts: List[Tensor],
                 alphas: List[Tensor], betas: List[Tensor], cins: List[int],
                 splits: List[Tensor]) -> None:
@@ -356,6 +373,9 @@ def sa_mlp_max_(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor
     _run("pn2_sa_mlp_max_f32", _L.pn2_sa_mlp_max_f32,
          (src, layers, n, 1, out.data_ptr(), out.stride(-2), 0 if ws is None else ws.data_ptr(),
           ws_bytes, _stream(points)), points.device, flops=flops)
+
+
+sa_mlp_max_ = torch.library.custom_op("pn2::sa_mlp_max_", sa_mlp_max_direct, mutates_args=("out",))
 
 
 @sa_mlp_max_.register_fake

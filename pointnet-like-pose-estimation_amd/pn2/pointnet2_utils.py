@@ -69,13 +69,13 @@ def _pack_chain(convs, bns, cache, rot0, xyz=0, xyz_first=True):
         with torch.no_grad():
             for li, (conv, bn) in enumerate(zip(convs, bns)):
                 rot = rot0 if li == 0 else 0
-                wt, al, be = ops.pack_layer(conv.weight, conv.bias, bn.weight, bn.bias,
+                wt, al, be = ops.pack_layer_direct(conv.weight, conv.bias, bn.weight, bn.bias,
                                             bn.running_mean, bn.running_var, float(bn.eps), rot)
                 wts.append(wt)
                 als.append(al)
                 bes.append(be)
                 cins.append(conv.weight.shape[1])
-                splits.append(ops.pack_layer_split(conv.weight, xyz if li == 0 else 0,
+                splits.append(ops.pack_layer_split_direct(conv.weight, xyz if li == 0 else 0,
                                                    xyz_first))
         cache["key"] = key
         cache["layers"] = (wts, als, bes, cins, splits)
@@ -104,35 +104,36 @@ def _torch_mlp_max(grouped, convs, bns):
 def square_distance(src, dst):
     """pointnet2_utils.py:5-26 -> [B, N, M], bit-identical to the reference's float32 result."""
     C = src.shape[-1]
-    return ops.square_distance(ops.pack_points(src), ops.pack_points(dst), C)
+    return ops.square_distance_direct(ops.pack_points_direct(src), ops.pack_points_direct(dst), C)
 
 
 def index_points(points, idx):
     """pointnet2_utils.py:28-45: points [B,N,C], idx [B, ...] -> [B, ..., C]."""
     B = points.shape[0]
-    out = ops.index_points(points, idx.reshape(B, -1))
+    out = ops.index_points_direct(points, idx.reshape(B, -1))
     return out.view(*idx.shape, points.shape[-1])
 
 
 def farthest_point_sample(points, number):
     """pointnet2_utils.py:47-68: [B,N,C] -> [B, number] int64 (consumes one CPU randint)."""
     B, N, _ = points.shape
-    return ops.fps(points, number, _draw_start(B, N, points.device))[0]
+    return ops.fps_direct(points, number, _draw_start(B, N, points.device))[0]
 
 
 def query_ball_point(radius, number, points, new_points):
     """pointnet2_utils.py:70-90: [B,S,number] int64; IndexError if number > N (as the
     reference)."""
     C = points.shape[-1]
-    return ops.ball_query(ops.pack_points(points), ops.pack_points(new_points), C, radius, number)
+    return ops.ball_query_direct(ops.pack_points_direct(points), ops.pack_points_direct(new_points),
+                                 C, radius, number)
 
 
 def sample_and_group(points, feature, point_number, sample_number, radius, returnfps=False):
     """pointnet2_utils.py:92-120.  points [B,N,C], feature [B,N,D] or None."""
     B, N, C = points.shape
-    fps_idx, new_points, cpk, ppk = ops.fps(points, point_number, _draw_start(B, N, points.device))
-    idx = ops.ball_query(ppk, cpk, C, radius, sample_number)
-    new_feature = ops.group(points, feature, new_points, idx, False)
+    fps_idx, new_points, cpk, ppk = ops.fps_direct(points, point_number, _draw_start(B, N, points.device))
+    idx = ops.ball_query_direct(ppk, cpk, C, radius, sample_number)
+    new_feature = ops.group_direct(points, feature, new_points, idx, False)
     if returnfps:
         grouped = index_points(feature if feature is not None else points, idx)
         return new_points, new_feature, grouped, fps_idx
@@ -185,17 +186,22 @@ class PointNetSetAbstraction(nn.Module):
         dev = pts.device
         if self.group_all:
             out = torch.empty(B, cout, device=dev, dtype=torch.float32)
-            ops.sa_mlp_max_(out, _lib.SRC_GROUP_ALL, pts, feat, None, None, wts, als, bes, cins,
+            ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_ALL, pts, feat, None, None, wts, als, bes, cins,
                             splits)
             new_points = torch.zeros(B, C, 1, device=dev, dtype=torch.float32)
             return new_points, out.view(B, 1, cout).permute(0, 2, 1)
         S, K = self.point_number, self.sample_number
-        with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
-            _, new_points, cpk, ppk = ops.fps(pts, S, _draw_start(B, N, dev))
-            idx = ops.ball_query(ppk, cpk, C, self.radius, K)
-        span.finish([new_points], [new_points, idx])
+        pre = geometry.take(self, pts)  # FPS precomputed by pn2.pipeline
+        if pre is not None:
+            new_points, cpk, ppk = pre
+            idx = ops.ball_query_direct(ppk, cpk, C, self.radius, K)
+        else:
+            with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
+                _, new_points, cpk, ppk = ops.fps_direct(pts, S, _draw_start(B, N, dev))
+                idx = ops.ball_query_direct(ppk, cpk, C, self.radius, K)
+            span.finish([new_points], [new_points, idx])
         out = torch.empty(B * S, cout, device=dev, dtype=torch.float32)
-        ops.sa_mlp_max_(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
+        ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
                         cins, splits)
         return new_points.permute(0, 2, 1), out.view(B, S, cout).permute(0, 2, 1)
 
@@ -206,9 +212,9 @@ class PointNetSetAbstraction(nn.Module):
             new_points, grouped = sample_and_group_all(pts, feat)
         else:
             B, N, C = pts.shape
-            _, new_points, cpk, ppk = ops.fps(pts.detach(), self.point_number,
+            _, new_points, cpk, ppk = ops.fps_direct(pts.detach(), self.point_number,
                                               _draw_start(B, N, pts.device))
-            idx = ops.ball_query(ppk, cpk, C, self.radius, self.sample_number)
+            idx = ops.ball_query_direct(ppk, cpk, C, self.radius, self.sample_number)
             grouped = _torch_group(pts, idx, new_points, feat, False)
         return new_points.permute(0, 2, 1), _torch_mlp_max(grouped, self.mlp_convs, self.mlp_bns)
 
@@ -249,17 +255,23 @@ class PointNetSetAbstractionMsg(nn.Module):
                               False)
                   for i in range(len(self.radius_list))]
         total = sum(ch[0][-1].shape[1] for ch in chains)
-        with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
-            _, new_points, cpk, ppk = ops.fps(pts, S, _draw_start(B, N, dev))
-            idxs = [ops.ball_query(ppk, cpk, C, r, k)
+        pre = geometry.take(self, pts)  # FPS precomputed by pn2.pipeline
+        if pre is not None:
+            new_points, cpk, ppk = pre
+            idxs = [ops.ball_query_direct(ppk, cpk, C, r, k)
                     for r, k in zip(self.radius_list, self.sample_number_list)]
-        span.finish([new_points], [new_points] + idxs)
+        else:
+            with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
+                _, new_points, cpk, ppk = ops.fps_direct(pts, S, _draw_start(B, N, dev))
+                idxs = [ops.ball_query_direct(ppk, cpk, C, r, k)
+                        for r, k in zip(self.radius_list, self.sample_number_list)]
+            span.finish([new_points], [new_points] + idxs)
         out = torch.empty(B * S, total, device=dev, dtype=torch.float32)
         col = 0
         for i, idx in enumerate(idxs):
             wts, als, bes, cins, splits = chains[i]
             cout = wts[-1].shape[1]
-            ops.sa_mlp_max_(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
+            ops.sa_mlp_max_direct(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
                             new_points, idx, wts, als, bes, cins, splits)
             col += cout
         return new_points.permute(0, 2, 1), out.view(B, S, total).permute(0, 2, 1)
@@ -268,11 +280,11 @@ class PointNetSetAbstractionMsg(nn.Module):
         pts = points.permute(0, 2, 1)
         feat = None if feature is None else feature.permute(0, 2, 1)
         B, N, C = pts.shape
-        _, new_points, cpk, ppk = ops.fps(pts.detach(), self.point_number,
+        _, new_points, cpk, ppk = ops.fps_direct(pts.detach(), self.point_number,
                                           _draw_start(B, N, pts.device))
         outs = []
         for i, radius in enumerate(self.radius_list):
-            idx = ops.ball_query(ppk, cpk, C, radius, self.sample_number_list[i])
+            idx = ops.ball_query_direct(ppk, cpk, C, radius, self.sample_number_list[i])
             grouped = _torch_group(pts, idx, new_points, feat, True)
             outs.append(_torch_mlp_max(grouped, self.conv_blocks[i], self.bn_blocks[i]))
         return new_points.permute(0, 2, 1), torch.cat(outs, dim=1)

@@ -88,3 +88,29 @@ def test_sa_mlp_vs_oracle(case, path, monkeypatch):
     grouped = oracle.group(ps, feat, idx, ctr, feature_first=msg)
     want = oracle.mlp_max(grouped, _oracle_layers(convs, bns))
     _close(newf.permute(0, 2, 1).cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("case", [0, 1, 2, 4])
+def test_sa_mlp_deterministic(case):
+    """Repeated calls on the same inputs give the same bits (no race in the kernels' staging)."""
+    import pn2
+    C, D, K, S, N, mlp, msg, _ = CASES[case]
+    B, radius = 4, 0.35
+    pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 300 + case)
+    feat = torch.randn(B, N, D, generator=torch.Generator().manual_seed(case)) if D else None
+    torch.manual_seed(case)
+    if msg:
+        sa = pn2.PointNetSetAbstractionMsg(S, [K], [radius], D, [mlp])
+    else:
+        sa = pn2.PointNetSetAbstraction(S, K, radius, C + D, mlp)
+    cases.randomize_bn(sa, case)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous().to(DEV)
+    f = feat.permute(0, 2, 1).contiguous().to(DEV) if D else None
+    outs = []
+    for _ in range(6):
+        torch.manual_seed(7)
+        with torch.no_grad():
+            outs.append(sa(x, f)[1].cpu().numpy())
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])

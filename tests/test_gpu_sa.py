@@ -268,3 +268,48 @@ def test_graph_replay_matches_eager(head):
     for g, w in zip(got, want):
         np.testing.assert_array_equal(g, w)
     np.testing.assert_array_equal(rng_got.numpy(), rng_want.numpy())
+
+
+@pytest.mark.parametrize("head", ["ClsSSG", "ClsMSG", "TranslationSSG"])
+def test_pipelined_forward_matches_eager(head):
+    """pn2.pipeline.PipelinedForward (FPS of batch i+1 on its own CUs while batch i runs) returns
+    the eager forwards' results for a sequence of batches -- including a sharded call -- and
+    leaves the CPU generator where the eager sequence leaves it.  Every SA output (the l3
+    feature) is bit-identical; the head's Linear layers go through torch's BLAS, which may pick
+    another GEMM kernel on the CU-restricted stream, so logits are held to 1e-6 relative."""
+    from pn2 import heads as H
+    from pn2 import shard
+    from pn2.pipeline import PipelinedForward
+    torch.manual_seed(8)
+    model = getattr(H, head)().eval()
+    cases.randomize_bn(model, 8)
+    model = model.to(DEV)
+    kind = "onehot10" if head.startswith("Translation") else "uniform3"
+    B, N = (8, 2048) if head == "ClsMSG" else (16, 1024)
+    xs = [cases.cloud(kind, B, N, 90 + i).permute(0, 2, 1).contiguous().to(DEV) for i in range(4)]
+    extras = None
+    if head.startswith("Translation"):
+        extras = [(torch.randn(B, 3, generator=torch.Generator().manual_seed(i)).to(DEV),) for i in range(4)]
+
+    feats = []
+    last_sa = model.sa3 if hasattr(model, "sa3") else model.sa2
+    last_sa.register_forward_hook(lambda m, i, o: feats.append(o[1].cpu().numpy()))
+
+    def first(o):
+        return (o[0] if isinstance(o, tuple) else o).cpu().numpy()
+
+    torch.manual_seed(31)
+    with torch.no_grad(), shard.batch_shard(2 * B, B):
+        want = [first(model(x, *(extras[i] if extras else ()))) for i, x in enumerate(xs)]
+    rng_want = torch.randint(0, 1 << 30, (4,))
+    want_f, feats[:] = list(feats), []
+    torch.manual_seed(31)
+    with shard.batch_shard(2 * B, B):
+        got = [first(o) for o in PipelinedForward(model, geometry_cus=16).run(xs, extras)]
+    rng_got = torch.randint(0, 1 << 30, (4,))
+    np.testing.assert_array_equal(rng_got.numpy(), rng_want.numpy())
+    assert len(feats) == len(want_f) == len(xs)
+    for g, w in zip(feats, want_f):
+        np.testing.assert_array_equal(g, w)
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g, w, rtol=1e-6, atol=1e-6 * float(np.abs(w).max()))
