@@ -29,15 +29,12 @@
 //             group spans several slabs (ReLU output >= +0: uint order == float order).
 // Weights stream from L2 (1 KB per fragment and plane, shared by every wave on the chip).
 #include "pn2_internal.h"
+#include "split_bf16.h"
 
 #include <cstdlib>
 #include <cstring>
 
 namespace pn2 {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float cfloatx16 __attribute__((ext_vector_type(16)));
-typedef float cfloatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kChainWaves = 4;
 constexpr int kChainRows = 32 * kChainWaves;
@@ -61,50 +58,6 @@ struct ChainArgs {
     int lds_bn;    // byte offset of the staged BN scale/shift
     int lds_ring;  // byte offset of the per-wave weight rings
 };
-
-struct Split {
-    bf16x8 h, m, l;
-};
-
-__device__ __forceinline__ float chain_relu(float t) { return t > 0.f ? t : 0.f; }  // never -0
-
-__device__ __forceinline__ Split split8(const float (&x)[8]) {
-    Split s;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const __bf16 a = (__bf16)x[j];
-        const float r = x[j] - (float)a;
-        const __bf16 b = (__bf16)r;
-        const float r2 = r - (float)b;
-        s.h[j] = a;
-        s.m[j] = b;
-        s.l[j] = (__bf16)r2;
-    }
-    return s;
-}
-
-#define PN2_MFMA16 __builtin_amdgcn_mfma_f32_32x32x16_bf16
-// acc += a * b with both operands split (6 bf16 products).  The weight operand's planes are
-// consumed in the order they are read from the ring (hi, mid, lo), so the first products can
-// start while the later planes are still in flight.
-__device__ __forceinline__ cfloatx16 mma6_wa(const Split &w, const Split &x, cfloatx16 acc) {
-    acc = PN2_MFMA16(w.h, x.h, acc, 0, 0, 0);
-    acc = PN2_MFMA16(w.h, x.m, acc, 0, 0, 0);
-    acc = PN2_MFMA16(w.h, x.l, acc, 0, 0, 0);
-    acc = PN2_MFMA16(w.m, x.h, acc, 0, 0, 0);
-    acc = PN2_MFMA16(w.m, x.m, acc, 0, 0, 0);
-    acc = PN2_MFMA16(w.l, x.h, acc, 0, 0, 0);
-    return acc;
-}
-__device__ __forceinline__ cfloatx16 mma6_wb(const Split &x, const Split &w, cfloatx16 acc) {
-    acc = PN2_MFMA16(x.h, w.h, acc, 0, 0, 0);
-    acc = PN2_MFMA16(x.m, w.h, acc, 0, 0, 0);
-    acc = PN2_MFMA16(x.l, w.h, acc, 0, 0, 0);
-    acc = PN2_MFMA16(x.h, w.m, acc, 0, 0, 0);
-    acc = PN2_MFMA16(x.m, w.m, acc, 0, 0, 0);
-    acc = PN2_MFMA16(x.h, w.l, acc, 0, 0, 0);
-    return acc;
-}
 
 __device__ __forceinline__ Split load_w(const ChainLayer &L, int t, int kb, int lane) {
     const int64_t plane = (int64_t)L.tiles * L.kb * 64;
@@ -143,7 +96,6 @@ __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const floa
 // R-1 steps ahead of use into this wave's own ring of R slots: no cross-wave barrier, and the
 // only vector-memory traffic in flight is the ring (BN parameters are staged in LDS), so a
 // counted s_waitcnt vmcnt retires exactly the step about to be read.
-typedef __attribute__((address_space(3))) void lds_void;
 constexpr int kStepBytes = 3 * 1024;
 
 // frag: the step's plane-0 fragment (wave-uniform); loff = lane * 16 -- the uniform-base +
@@ -156,14 +108,7 @@ __device__ __forceinline__ void ring_issue(const bf16x8 *frag, int64_t plane, ch
                                          (lds_void *)(slot + p * 1024), 16, 0, 0);
 }
 
-__device__ __forceinline__ Split ring_read(const char *slot, int lane) {
-    const bf16x8 *q = reinterpret_cast<const bf16x8 *>(slot) + lane;
-    Split w;
-    w.h = q[0];
-    w.m = q[64];
-    w.l = q[128];
-    return w;
-}
+
 
 // Step j refills the slot of step j-1 before waiting for its own copies, so NR-1 later steps
 // are in flight at every wait (issues past the end repeat the last step into an
@@ -181,10 +126,7 @@ __device__ __forceinline__ void ring_wait() {
 // the memory clobber also keeps those reads from being scheduled after the refill.
 __device__ __forceinline__ void ring_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// lanes l and l^32 exchange x (the two halves of a 32x32 tile column)
-__device__ __forceinline__ float swap_halves(float x) {
-    return __shfl_xor(x, 32);
-}
+
 
 // KB0M > 0: the layer-0 input (<= KB0M k-blocks) is gathered once into registers and layer 0 runs
 // tile by tile from the ring like layers 1 and 2; KB0M == 0: layer 0 streams its input blocks

@@ -1,0 +1,322 @@
+// sa_dense.hip -- one wide shared-MLP layer as a split-bf16 GEMM on gfx950: the group_all SA
+// layer (PointNetSetAbstraction with group_all=True, /root/reference/model/pointnet2_utils.py
+// :163-172 over sample_and_group_all :122-141) and any chain too wide for the register-resident
+// kernel run layer by layer through an HBM workspace with it.
+//
+//   out = relu(alpha * (A . W^T) + beta)            (optionally max-pooled over K-row groups)
+//
+// Workgroup: 4 waves, 128 rows x NTC 32-column tiles; wave w owns rows 32w..32w+31 (standard
+// MFMA orientation: A = activations, lane = row; B = weights, lane = output column).
+//   A   each lane loads its row's 16-channel k-block (two 16-byte runs) straight from HBM/L2 --
+//       the previous layer's fp32 rows, or for group_all's first layer the [xyz | features] of
+//       the point (split layout: block 0 = xyz, blocks >= 1 = features) -- splits it once and
+//       feeds all NTC column tiles with it.  A for the next stage is loaded before the stage's
+//       weight DMA is issued, so waiting for it never waits for the DMA.
+//   B   the workgroup's weight fragments (3 planes x NTC tiles x kKC k-blocks = one stage) are
+//       copied to LDS once by global_load_lds, double-buffered, one barrier per stage.
+//   out dense rows (row-major, coalesced per row), or the max over each group of K rows: in
+//       registers, then across the workgroup's waves in LDS (K | 128), or by atomicMax on the
+//       float bits into a zeroed output (ReLU output >= +0: uint order == float order).
+#include "pn2_internal.h"
+#include "split_bf16.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+namespace pn2 {
+
+constexpr int kDW = 4;            // waves per workgroup
+constexpr int kDRows = 32 * kDW;  // rows per workgroup
+constexpr int kKC = 4;            // k-blocks per weight stage
+
+struct DenseSplitArgs {
+    int mode;  // 0: rows [M][rs] fp32; 1: group_all points (row R = point R % N of cloud R / N)
+    const float *rows;
+    int64_t rs;
+    const float *pts;
+    int64_t pb, pn, pc;
+    const float *feat;
+    int64_t fb, fn;
+    int N, C, D;  // group_all: points per cloud, xyz channels, feature channels
+    int cin;      // rows mode: valid input channels
+    int vec;      // 16-byte loads of feature / row runs are allowed
+    const bf16x8 *w;
+    const float *alpha, *beta;
+    int kb, tiles;  // k-blocks of the input, 32-column tiles of the output
+    int M;
+    int pool;       // 0: out[row][col]; 1: out[group][col] = max over K rows
+    int K;
+    int pool_mode;  // 0: registers (K = 8, 16), 1: LDS (K | kDRows), 2: HBM atomics
+    float *out;
+    int64_t ostride;
+};
+
+template <int NTC>
+__global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    constexpr int kFrag = 3 * NTC;                   // fragments per k-block
+    constexpr int kStage = kKC * kFrag * 1024;       // bytes per weight stage
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int row0 = blockIdx.x * kDRows;
+    const int ct0 = blockIdx.y * NTC;  // first output tile
+    const int ncols = 32 * NTC;
+    char *stages = dsm;
+    float *opool = reinterpret_cast<float *>(dsm + 2 * kStage);  // [groups][ncols]
+    const int gpb = A.pool_mode == 1 ? kDRows / A.K : 0;
+    if (A.pool_mode == 1)
+        for (int e = tid; e < gpb * ncols; e += 64 * kDW) opool[e] = 0.f;
+
+    // ---- this lane's row (A operand)
+    const int R = row0 + 32 * wave + r;
+    const bool valid = R < A.M;
+    const float *arow = nullptr, *frow = nullptr, *prow = nullptr;
+    if (A.mode == 0) {
+        arow = A.rows + (int64_t)(valid ? R : 0) * A.rs;
+    } else {
+        const int b = (valid ? R : 0) / A.N, n = (valid ? R : 0) - b * A.N;
+        prow = A.pts + (int64_t)b * A.pb + (int64_t)n * A.pn;
+        if (A.feat) frow = A.feat + (int64_t)b * A.fb + (int64_t)n * A.fn;
+    }
+    // lane (r, h) holds channels 16kb + (j&3) + 8(j>>2) + 4h of its row in element j
+    auto load_a = [&](int kb, float (&x)[8]) {
+        if (!valid || kb >= A.kb) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = 0.f;
+            return;
+        }
+        if (A.mode == 1 && kb == 0) {  // raw xyz (sample_and_group_all does not centre)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int ch = (j & 3) + 8 * (j >> 2) + 4 * h;
+                x[j] = ch < A.C ? prow[(int64_t)ch * A.pc] : 0.f;
+            }
+            return;
+        }
+        const float *src = A.mode == 0 ? arow : frow;
+        const int lim = A.mode == 0 ? A.cin : A.D;
+        const int base = A.mode == 0 ? 16 * kb : 16 * (kb - 1);
+#pragma unroll
+        for (int run = 0; run < 2; ++run) {
+            const int f = base + 8 * run + 4 * h;
+            if (A.vec) {
+                cfloatx4 q = {0.f, 0.f, 0.f, 0.f};
+                if (f < lim) q = *reinterpret_cast<const cfloatx4 *>(src + f);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[4 * run + i] = q[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[4 * run + i] = f + i < lim ? src[f + i] : 0.f;
+            }
+        }
+    };
+
+    // ---- weight stages: stage c = k-blocks [c*kKC, c*kKC + kKC) of this workgroup's NTC tiles,
+    // fragment (kbl, i, p) at ((kbl * NTC + i) * 3 + p) KB
+    const int nst = (A.kb + kKC - 1) / kKC;
+    const int64_t plane = (int64_t)A.tiles * A.kb * 64;
+    const unsigned loff = (unsigned)lane * 16u;
+    auto issue_stage = [&](int c) {
+        char *buf = stages + (c & 1) * kStage;
+        for (int f = wave; f < kKC * kFrag; f += kDW) {
+            const int kbl = f / kFrag, rem = f - kbl * kFrag;
+            const int i = rem / 3, p = rem - 3 * i;
+            const int kb = min(c * kKC + kbl, A.kb - 1);
+            const bf16x8 *src = A.w + p * plane + ((int64_t)(ct0 + i) * A.kb + kb) * 64;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const char *>(src) + loff,
+                                             (lds_void *)(buf + f * 1024), 16, 0, 0);
+        }
+    };
+
+    cfloatx16 acc[NTC];
+#pragma unroll
+    for (int i = 0; i < NTC; ++i)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][q] = 0.f;
+    float xa[kKC][8];
+#pragma unroll
+    for (int k = 0; k < kKC; ++k) load_a(k, xa[k]);
+    issue_stage(0);
+    for (int c = 0; c < nst; ++c) {
+        __syncthreads();  // stage c landed for every wave; buffer (c+1)&1 is free again
+        float xn[kKC][8];
+#pragma unroll
+        for (int k = 0; k < kKC; ++k) load_a((c + 1) * kKC + k, xn[k]);
+        if (c + 1 < nst) issue_stage(c + 1);
+        const char *buf = stages + (c & 1) * kStage;
+#pragma unroll
+        for (int k = 0; k < kKC; ++k) {
+            if (c * kKC + k < A.kb) {
+                const Split xs = split8(xa[k]);
+#pragma unroll
+                for (int i = 0; i < NTC; ++i)
+                    acc[i] = mma6_wb(xs, ring_read(buf + (k * kFrag + 3 * i) * 1024, lane), acc[i]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kKC; ++k)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xa[k][j] = xn[k][j];
+    }
+
+    // ---- epilogue: lane = output column, register q = row (q&3) + 8(q>>2) + 4h of the slab
+    const int slab_row = row0 + 32 * wave;
+    const unsigned G = A.pool ? (unsigned)A.M / (unsigned)A.K : 0u;
+#pragma unroll
+    for (int i = 0; i < NTC; ++i) {
+        const int col = 32 * (ct0 + i) + r;
+        const float al = A.alpha[col], be = A.beta[col];
+        if (!A.pool) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = slab_row + (q & 3) + 8 * (q >> 2) + 4 * h;
+                if (row < A.M) A.out[(int64_t)row * A.ostride + col] = chain_relu(__builtin_fmaf(acc[i][q], al, be));
+            }
+            continue;
+        }
+        // max over rows of relu(fma(acc, al, be)) = relu(fma(row max (al >= 0) or min, al, be))
+        const bool up = al >= 0.f;
+        auto fin = [&](float mx, float mn) { return chain_relu(__builtin_fmaf(up ? mx : mn, al, be)); };
+        if (A.pool_mode == 0) {  // K = 8 or 16: rows 8k..8k+7 are registers 4k..4k+3
+            float mx[4], mn[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                mx[k] = fmaxf(fmaxf(acc[i][4 * k], acc[i][4 * k + 1]), fmaxf(acc[i][4 * k + 2], acc[i][4 * k + 3]));
+                mn[k] = fminf(fminf(acc[i][4 * k], acc[i][4 * k + 1]), fminf(acc[i][4 * k + 2], acc[i][4 * k + 3]));
+                mx[k] = fmaxf(mx[k], swap_halves(mx[k]));
+                mn[k] = fminf(mn[k], swap_halves(mn[k]));
+            }
+            if (h == 0) {
+                const int per = A.K / 8;  // register groups per output group
+#pragma unroll
+                for (int k = 0; k < 4; k += 1) {
+                    if (k % per) continue;
+                    float a = mx[k], z = mn[k];
+                    if (per == 2) a = fmaxf(a, mx[k + 1]), z = fminf(z, mn[k + 1]);
+                    const unsigned gg = (unsigned)(slab_row + 8 * k) / (unsigned)A.K;
+                    if (gg < G) A.out[(int64_t)gg * A.ostride + col] = fin(a, z);
+                }
+            }
+            continue;
+        }
+        float mx = acc[i][0], mn = acc[i][0];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) {
+            mx = fmaxf(mx, acc[i][q]);
+            mn = fminf(mn, acc[i][q]);
+        }
+        const float m = fin(fmaxf(mx, swap_halves(mx)), fminf(mn, swap_halves(mn)));
+        if (h == 0 && slab_row < A.M) {
+            const unsigned gg = (unsigned)slab_row / (unsigned)A.K;
+            if (A.pool_mode == 1)
+                atomicMax(reinterpret_cast<unsigned *>(opool) + ((int)gg - row0 / A.K) * ncols + 32 * i + r,
+                          __float_as_uint(m));
+            else
+                atomicMax(reinterpret_cast<unsigned *>(A.out + (int64_t)gg * A.ostride + col), __float_as_uint(m));
+        }
+    }
+    if (A.pool && A.pool_mode == 1) {
+        __syncthreads();
+        for (int e = tid; e < gpb * ncols; e += 64 * kDW) {
+            const int gl = e / ncols, c = e - gl * ncols;
+            const unsigned gg = (unsigned)(row0 / A.K + gl);
+            if (gg < G) A.out[(int64_t)gg * A.ostride + 32 * ct0 + c] = opool[e];
+        }
+    }
+}
+
+template <int NTC>
+static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
+    const size_t lds = (size_t)2 * kKC * 3 * NTC * 1024 +
+                       (A.pool_mode == 1 ? (size_t)(kDRows / A.K) * 32 * NTC * 4 : 0);
+    dim3 grid((unsigned)((A.M + kDRows - 1) / kDRows), (unsigned)(A.tiles / NTC));
+    hipLaunchKernelGGL(dense_split_kernel<NTC>, grid, dim3(64 * kDW), lds, st, A);
+    PN2_LAUNCH_CHECK("dense_split_kernel");
+    return PN2_OK;
+}
+
+static int dense_split_layer(DenseSplitArgs &A, hipStream_t st) {
+    // two output tiles per wave when that still leaves >= 2 workgroups per CU
+    const int64_t rowblocks = (A.M + kDRows - 1) / kDRows;
+    const int ntc = (A.tiles % 2 == 0 && rowblocks * (A.tiles / 2) >= 512) ? 2 : 1;
+    if (A.pool) {
+        if (A.K == 8 || A.K == 16) A.pool_mode = 0;
+        else if (A.K % 32 == 0 && kDRows % A.K == 0) A.pool_mode = 1;
+        else A.pool_mode = 2;
+        if (A.pool_mode == 2) {
+            const int64_t G = A.M / A.K, cols = 32 * (int64_t)A.tiles;
+            hipError_t e = A.ostride == cols
+                               ? hipMemsetAsync(A.out, 0, (size_t)G * cols * 4, st)
+                               : hipMemset2DAsync(A.out, (size_t)A.ostride * 4, 0, (size_t)cols * 4, (size_t)G, st);
+            if (e != hipSuccess) return set_error(PN2_EHIP, "dense_split: memset: %s", hipGetErrorString(e));
+        }
+    }
+    return ntc == 2 ? launch_dense_split<2>(A, st) : launch_dense_split<1>(A, st);
+}
+
+// Widest hidden layer of a chain the split dense path runs layer by layer (0: not eligible).
+int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers) {
+    if (getenv("PN2_MLP_PATH") && strcmp(getenv("PN2_MLP_PATH"), "f32") == 0) return 0;
+    if (s.mode != PN2_SRC_GROUP_ALL && s.mode != PN2_SRC_ROWS) return 0;
+    if (s.mode == PN2_SRC_GROUP_ALL && s.C > 16) return 0;
+    int64_t w = 0;
+    for (int l = 0; l < nlayers; ++l) {
+        if (!layers[l].wt_split || ((uintptr_t)layers[l].wt_split & 15)) return 0;
+        if (l < nlayers - 1) w = std::max(w, layers[l].cout);
+    }
+    return nlayers > 1 ? (w + 3) / 4 * 4 : 1;
+}
+
+// 1: launched, 0: not eligible, <0: error.  Layers run one by one; hidden outputs ping-pong
+// through the two [M][w] halves of the workspace.
+int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
+                           float *out, int64_t ostride, float *ws, int64_t ws_bytes, int64_t M,
+                           int64_t K, hipStream_t st) {
+    const int64_t w = dense_split_width(s, layers, nlayers);
+    if (w == 0) return 0;
+    if (nlayers > 1 && (!ws || ws_bytes < 2 * M * w * 4 || ((uintptr_t)ws & 15))) return 0;
+    const bool vec_rows_ok = true;
+    for (int l = 0; l < nlayers; ++l) {
+        const bool last = l == nlayers - 1;
+        DenseSplitArgs A;
+        memset(&A, 0, sizeof(A));
+        if (l == 0 && s.mode == PN2_SRC_GROUP_ALL) {
+            A.mode = 1;
+            A.pts = s.pts; A.pb = s.pb; A.pn = s.pn; A.pc = s.pc;
+            A.feat = s.feat; A.fb = s.fb; A.fn = s.fn;
+            A.N = (int)s.N; A.C = (int)s.C; A.D = (int)s.D;
+            A.vec = (s.D == 0 || (s.D % 4 == 0 && ((uintptr_t)s.feat & 15) == 0 && s.fn % 4 == 0 &&
+                                  s.fb % 4 == 0)) ? 1 : 0;
+            A.kb = (int)pn2_layer_split_kblocks(layers[0].cin, s.C);
+        } else {
+            A.mode = 0;
+            if (l == 0) {
+                A.rows = s.rows;
+                A.rs = s.rs;
+            } else {
+                A.rows = ws + ((l - 1) & 1) * M * w;
+                A.rs = w;
+            }
+            A.cin = (int)layers[l].cin;
+            A.vec = (vec_rows_ok && ((uintptr_t)A.rows & 15) == 0 && A.rs % 4 == 0) ? 1 : 0;
+            A.kb = (int)((layers[l].cin + 15) / 16);
+        }
+        A.w = reinterpret_cast<const bf16x8 *>(layers[l].wt_split);
+        A.alpha = layers[l].alpha;
+        A.beta = layers[l].beta;
+        A.tiles = (int)(layers[l].cout / 32);
+        A.M = (int)M;
+        A.pool = last ? pool : 0;
+        A.K = (int)K;
+        A.out = last ? out : ws + (l & 1) * M * w;
+        A.ostride = last ? ostride : w;
+        const int rc = dense_split_layer(A, st);
+        if (rc != PN2_OK) return rc;
+    }
+    return 1;
+}
+
+}  // namespace pn2

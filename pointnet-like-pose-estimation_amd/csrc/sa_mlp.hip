@@ -846,7 +846,8 @@ extern "C" int64_t pn2_sa_mlp_workspace_bytes(const pn2_sa_src *src, const pn2_m
                                               int nlayers) {
     int64_t M = 0, K = 1;
     if (validate(src, layers, nlayers, M, K) != PN2_OK) return -1;
-    return 2 * M * workspace_width(*src, layers, nlayers, M, K) * 4;
+    const int64_t ds = nlayers > 1 ? dense_split_width(*src, layers, nlayers) : 0;
+    return 2 * M * std::max(ds, workspace_width(*src, layers, nlayers, M, K)) * 4;
 }
 
 static int run_plan(const pn2_sa_src &cur, const pn2_mlp_layer *layers, int l0, int l1, int pool,
@@ -877,6 +878,12 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
     if (pool) PN2_REQUIRE(M % K == 0, "pn2_sa_mlp_max_f32: rows not a multiple of the group size");
     hipStream_t st = as_stream(stream);
     rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, st);
+    if (rc != 0) {
+        if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
+        return rc < 0 ? rc : PN2_OK;
+    }
+    rc = try_launch_dense_split(*src, layers, nlayers, pool, out, ostride, workspace, workspace_bytes,
+                                M, K, st);
     if (rc != 0) {
         if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
         return rc < 0 ? rc : PN2_OK;

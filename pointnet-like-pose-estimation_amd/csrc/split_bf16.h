@@ -1,0 +1,78 @@
+// split_bf16.h -- fp32-accurate products on the bf16 matrix cores (gfx950), shared by the
+// register-resident chain kernel (sa_chain.hip) and the dense layer kernel (sa_dense.hip).
+//
+// An fp32 operand x is split into three bf16 planes x = h + m + l (round-to-nearest; the
+// residuals are exact in fp32, so the planes hold x to 2^-24 relative).  A product is taken as
+// hh + hm + mh + mm + hl + lh -- each an exact bf16 x bf16 product accumulated in fp32 by
+// v_mfma_f32_32x32x16_bf16 -- and the three dropped terms are <= 2^-23 of it: fp32-GEMM
+// accuracy at 6/16 of the fp32 MFMA cost.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace pn2 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float cfloatx16 __attribute__((ext_vector_type(16)));
+typedef float cfloatx4 __attribute__((ext_vector_type(4)));
+
+struct Split {
+    bf16x8 h, m, l;
+};
+
+__device__ __forceinline__ float chain_relu(float t) { return t > 0.f ? t : 0.f; }  // never -0
+
+__device__ __forceinline__ Split split8(const float (&x)[8]) {
+    Split s;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const __bf16 a = (__bf16)x[j];
+        const float r = x[j] - (float)a;
+        const __bf16 b = (__bf16)r;
+        const float r2 = r - (float)b;
+        s.h[j] = a;
+        s.m[j] = b;
+        s.l[j] = (__bf16)r2;
+    }
+    return s;
+}
+
+#define PN2_MFMA16 __builtin_amdgcn_mfma_f32_32x32x16_bf16
+// acc += a * b with both operands split (6 bf16 products).  The weight operand's planes are
+// consumed in the order they are read from the ring (hi, mid, lo), so the first products can
+// start while the later planes are still in flight.
+__device__ __forceinline__ cfloatx16 mma6_wa(const Split &w, const Split &x, cfloatx16 acc) {
+    acc = PN2_MFMA16(w.h, x.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.h, x.m, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.h, x.l, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.m, x.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.m, x.m, acc, 0, 0, 0);
+    acc = PN2_MFMA16(w.l, x.h, acc, 0, 0, 0);
+    return acc;
+}
+__device__ __forceinline__ cfloatx16 mma6_wb(const Split &x, const Split &w, cfloatx16 acc) {
+    acc = PN2_MFMA16(x.h, w.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.m, w.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.l, w.h, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.h, w.m, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.m, w.m, acc, 0, 0, 0);
+    acc = PN2_MFMA16(x.h, w.l, acc, 0, 0, 0);
+    return acc;
+}
+
+__device__ __forceinline__ Split ring_read(const char *slot, int lane) {
+    const bf16x8 *q = reinterpret_cast<const bf16x8 *>(slot) + lane;
+    Split w;
+    w.h = q[0];
+    w.m = q[64];
+    w.l = q[128];
+    return w;
+}
+
+// lanes l and l^32 exchange x (the two halves of a 32x32 tile column)
+__device__ __forceinline__ float swap_halves(float x) {
+    return __shfl_xor(x, 32);
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+}  // namespace pn2

@@ -179,7 +179,7 @@ class PointNetSetAbstraction(nn.Module):
         B, N, C = pts.shape
         # reference row order is [xyz, feature] (:114, :139); kernels use [feature, xyz]
         rot0 = C if feat is not None else 0
-        xyz = 0 if self.group_all else C  # the chain kernel serves the grouped layers
+        xyz = C  # split-bf16 rows are [xyz | features] for grouped and group_all layers alike
         wts, als, bes, cins, splits = _pack_chain(self.mlp_convs, self.mlp_bns, self._pack_cache,
                                                   rot0, xyz, True)
         cout = wts[-1].shape[1]

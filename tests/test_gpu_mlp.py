@@ -114,3 +114,43 @@ def test_sa_mlp_deterministic(case):
             outs.append(sa(x, f)[1].cpu().numpy())
     for o in outs[1:]:
         np.testing.assert_array_equal(o, outs[0])
+
+
+# group_all SA layers (sample_and_group_all + MLP + max over every point, pointnet2_utils.py
+# :122-141, :163-172): (C, D, N points = K, mlp, split kernel expected)
+GROUP_ALL = [
+    (3, 256, 128, [256, 512, 1024], True),   # SSG sa3 (LDS pool)
+    (10, 128, 512, [256, 512, 1024], True),  # translation_ssg sa2 (HBM atomics pool)
+    (3, 13, 64, [64, 96], True),             # unaligned features, 2 layers
+    (3, 0, 16, [64], True),                  # xyz only, one layer, register pool
+]
+
+
+@pytest.mark.parametrize("path", ["split", "f32"])
+@pytest.mark.parametrize("case", range(len(GROUP_ALL)))
+def test_group_all_vs_oracle(case, path, monkeypatch):
+    import pn2
+    from pn2 import _lib
+    C, D, N, mlp, split_ok = GROUP_ALL[case]
+    if path == "f32":
+        monkeypatch.setenv("PN2_MLP_PATH", "f32")
+    else:
+        monkeypatch.delenv("PN2_MLP_PATH", raising=False)
+    B = 3
+    pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 400 + case)
+    feat = torch.randn(B, N, D, generator=torch.Generator().manual_seed(500 + case)) if D else None
+    torch.manual_seed(case)
+    sa = pn2.PointNetSetAbstraction(None, None, None, C + D, mlp, True)
+    cases.randomize_bn(sa, case)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous().to(DEV)
+    f = feat.permute(0, 2, 1).contiguous().to(DEV) if D else None
+    with torch.no_grad():
+        newp, newf = sa(x, f)
+    torch.cuda.synchronize()
+    want_path = _lib.PATH_SPLIT_BF16 if (split_ok and path == "split") else _lib.PATH_F32
+    assert _lib.load().pn2_sa_mlp_last_path() == want_path
+    assert newp.shape == (B, C, 1) and float(newp.abs().sum()) == 0.0
+    rows = pts.numpy() if feat is None else np.concatenate([pts.numpy(), feat.numpy()], -1)
+    want = oracle.mlp_max(rows[:, None], _oracle_layers(sa.mlp_convs, sa.mlp_bns))  # [B, 1, cout]
+    _close(newf.permute(0, 2, 1).cpu().numpy(), want)
