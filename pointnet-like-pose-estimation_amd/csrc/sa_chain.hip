@@ -160,8 +160,8 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     __syncthreads();
     char *ring = csm + A.lds_ring + wave * (NR * kStepBytes);
     const unsigned loff = (unsigned)lane * 16u;
-    // Ring steps in consumption order: layer 0 (resident input) block-major, then layers 1 and
-    // 2 tile-major.  Step j first refills the previous step's slot with step j+NR-1 (after
+    // Ring steps in consumption order: layers 0 (resident input) and 1 block-major, layer 2
+    // tile-major.  Step j first refills the previous step's slot with step j+NR-1 (after
     // ring_fence), then waits for and reads its own; source addresses come from scalar
     // arithmetic on the layer's base (compile-time inside the unrolled loops), and past the end
     // the last step repeats into an already-consumed slot.
@@ -175,8 +175,8 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         z = min(z, L2.tiles * KB2 - 1);
         issue_l(L2, z / KB2, z % KB2);
     };
-    auto issue1 = [&](int y) {  // layer-1 step y
-        if (y < T1 * KB1) issue_l(L1, y / KB1, y % KB1);
+    auto issue1 = [&](int y) {  // layer-1 step y (block-major)
+        if (y < T1 * KB1) issue_l(L1, y % T1, y / T1);
         else issue2(y - T1 * KB1);
     };
     const int n0 = T0 * L0.kb;
@@ -288,20 +288,25 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         for (int t = 0; t < T0; ++t) hidden_epilogue(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
     }
 
-    // ---- layer 1: input in registers, one output tile at a time (transposed)
+    // ---- layer 1: input in registers, k-outer (each input block dies after its use, so X1 and
+    // X2 are never both whole in registers), every output tile accumulating (transposed)
     Split X2[2 * T1];
+    {
+        cfloatx16 acc[T1];
 #pragma unroll
-    for (int t = 0; t < T1; ++t) {
-        cfloatx16 acc;
+        for (int t = 0; t < T1; ++t)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+            for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < KB1; ++kb) {
-            ring_fence();
-            issue1(t * KB1 + kb + NR - 1);
-            acc = mma6_wa(read_w(), X1[kb], acc);
-        }
-        hidden_epilogue(acc, al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
+        for (int kb = 0; kb < KB1; ++kb)
+#pragma unroll
+            for (int t = 0; t < T1; ++t) {
+                ring_fence();
+                issue1(kb * T1 + t + NR - 1);
+                acc[t] = mma6_wa(read_w(), X1[kb], acc[t]);
+            }
+#pragma unroll
+        for (int t = 0; t < T1; ++t) hidden_epilogue(acc[t], al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
     }
 
     // ---- layer 2: standard orientation, pooled over the neighbourhood

@@ -8,7 +8,7 @@ FETCH_SIZE is reported in KB and counts half the bytes of wide coalesced reads o
     python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --config ssg
 
 Writes profiles/pmc_traffic.json[config] = {"pn2_sa_mlp_max_f32": bytes per API call (sum over
-the sa_mlp_kernel / dense_layer_kernel dispatches one call issues), "kernels": {name: {...}}}.
+the MLP kernel dispatches one call issues), "kernels": {name: {...}}}.
 bench.py reads the per-call figure into roofline.traffic.
 """
 import argparse
@@ -21,7 +21,9 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # pn2_sa_mlp_max_f32 calls per forward for each bench config (SSG: sa1, sa2, sa3)
 CALLS_PER_FORWARD = {"ssg": 3, "msg": 7, "pose": 6, "stress": 3}
-FORWARD_MARKER = "fps_kernel"  # first FPS of each forward: one per SA layer, counted below
+FORWARD_MARKER = "fps_kernel"  # one launch per sampled SA layer, counted below
+# kernels one pn2_sa_mlp_max_f32 call may dispatch
+MLP_KERNELS = ("sa_mlp_kernel", "dense_layer_kernel", "sa_chain_kernel", "dense_split_kernel")
 FPS_PER_FORWARD = {"ssg": 2, "msg": 2, "pose": 4, "stress": 2}
 
 
@@ -62,10 +64,10 @@ def main():
     n_fps = sum(len(v) for k, v in fetch.items() if FORWARD_MARKER in k)
     forwards = n_fps / FPS_PER_FORWARD[a.config]
     for name, v in fetch.items():
-        if "sa_mlp_kernel" in name or "dense_layer_kernel" in name:
+        if any(k in name for k in MLP_KERNELS):
             mlp_total += 2 * 1024 * sum(v)
     for name, v in write.items():
-        if "sa_mlp_kernel" in name or "dense_layer_kernel" in name:
+        if any(k in name for k in MLP_KERNELS):
             mlp_total += 1024 * sum(v)
     per_call = mlp_total / (forwards * CALLS_PER_FORWARD[a.config]) if forwards else None
     out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
