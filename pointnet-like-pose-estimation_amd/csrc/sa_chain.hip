@@ -27,7 +27,9 @@
 //             registers: the max over the neighbourhood is a register reduction (+ one lane
 //             exchange), merged across slabs in LDS (ds_max_u32) or HBM (atomicMax) when a
 //             group spans several slabs (ReLU output >= +0: uint order == float order).
-// Weights stream from L2 (1 KB per fragment and plane, shared by every wave on the chip).
+// Weights (3 KB per (tile, k-block) step: 1 KB fragment x 3 planes, L2-resident, shared by every
+// wave on the chip) are copied by global_load_lds into a small per-wave LDS ring a few steps
+// ahead of use (see ring_issue below); BN scale/shift are staged in LDS once per workgroup.
 #include "pn2_internal.h"
 #include "split_bf16.h"
 

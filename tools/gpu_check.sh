@@ -23,6 +23,16 @@ for s in $STEPS; do
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-timer ${BENCH_ARGS:-} > $OUT/prof.log 2>&1; ok $? prof
       find $OUT/prof -name "*kernel_stats.csv" | head -3 ;;
+    pmc)
+      # one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one gfx950 TCC pass);
+      # eager launch so every kernel runs on the full chip, as the kernel timer measures it
+      for c in FETCH_SIZE WRITE_SIZE; do
+        rm -rf $OUT/pmc_$c
+        timeout -k 10 300 rocprofv3 --pmc $c -d $OUT/pmc_$c -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timer --no-pipeline > $OUT/pmc_$c.log 2>&1; ok $? pmc_$c
+      done
+      python tools/pmc_traffic.py $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE --config ssg > $OUT/pmc_summary.txt 2>&1
+      cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
+      head -3 $OUT/pmc_summary.txt ;;
     *) echo "unknown step $s" ;;
   esac
 done
