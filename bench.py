@@ -66,6 +66,14 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline sample")
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the forward as a HIP graph")
+    ap.add_argument("--graph-pipeline", action="store_true",
+                    help="pipelined launch with every stage replayed from HIP graphs "
+                         "(pn2.pipeline.GraphedPipeline)")
+    ap.add_argument("--tail", action="store_true",
+                    help="eager pipelined: run the head on the geometry CUs after the last SA "
+                         "layer (see pn2.pipeline; default off)")
+    ap.add_argument("--no-tail", action="store_true",
+                    help="graph pipelined: keep the head on the compute stream")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="plain eager steps (default for single-head configs: pn2.pipeline)")
     ap.add_argument("--geometry-cus", type=int, default=32, help="CUs reserved for the FPS chain")
@@ -184,8 +192,13 @@ def main():
     pipelined = len(eager_models) == 1 and not a.graph and not a.no_pipeline
     pf = None
     if pipelined:
-        from pn2.pipeline import PipelinedForward
-        pf = PipelinedForward(eager_models[0], geometry_cus=a.geometry_cus)
+        from pn2.pipeline import GraphedPipeline, PipelinedForward
+        if a.graph_pipeline:
+            pf = GraphedPipeline(eager_models[0], geometry_cus=a.geometry_cus,
+                                 tail=not a.no_tail)
+        else:
+            pf = PipelinedForward(eager_models[0], geometry_cus=a.geometry_cus,
+                                  tail="auto" if a.tail else False)
 
     def run_pipelined(k):
         with shard.batch_shard(gB, lo):
@@ -273,7 +286,12 @@ def main():
                        "parallelism": "dp%d" % world},
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
             "launch": ("hip_graph" if a.graph else
-                       "pipelined(fps on %d CUs)" % a.geometry_cus if pipelined else "eager"),
+                       "%spipelined(fps%s on %d CUs)" % (
+                           "graphed " if a.graph_pipeline else "",
+                           " + head" if (a.graph_pipeline and not a.no_tail) or (
+                               a.tail and not names[0].startswith("translation")) else "",
+                           a.geometry_cus)
+                       if pipelined else "eager"),
             "eager_value": round(eager_value, 2),
         }
         print(json.dumps(line))

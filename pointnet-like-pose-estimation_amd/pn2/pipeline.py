@@ -9,6 +9,19 @@ latency-bound loop of one workgroup per cloud, so it gets a few dedicated CUs in
 time-sharing CUs with MFMA work (which slows its loop ~2.7x, measured), and the MFMA kernels
 keep the rest of the chip.
 
+The tail of each forward -- everything after the last SA layer returns (the FC head, `post`) --
+runs on a third stream with the geometry CUs: it is a dozen tiny launches (the head's largest
+GEMM has 2 workgroups) that would otherwise sit on the compute stream between batch i's last
+MLP and batch i+1's first, while the geometry CUs have room (FPS is ~45% of a step).  The switch
+is a forward hook on the last SA module, active only inside ``run``.  The last SA layer's
+outputs are handed over with ``record_stream``; any other compute-stream tensor the tail reads
+(e.g. the translation heads' ``mean``, computed before sa1 and added after the head) would not
+be, so ``tail="auto"`` uses it only for models called without extra inputs (every reference
+head but translation_*); ``tail=True`` forces it.  Off by default: with eager launches the host
+issue time per batch (~470 us at SSG B=32, measured) is as long as the compute stream's work,
+and the extra stream hops cost more than the tail frees (62.6k vs 66.0k clouds/s).  It pays in
+``GraphedPipeline`` (default on there).
+
 Results and RNG.  Every batch computes what ``model(x)`` computes: the SA layers run the same
 kernels and produce the same bits (test_pipelined_forward_matches_eager); the head's own
 ``nn.Linear`` layers go through torch's BLAS, which may choose a different GEMM kernel on the
@@ -33,14 +46,14 @@ from . import ops
 from . import shard
 from .pointnet2_utils import PointNetSetAbstraction, PointNetSetAbstractionMsg
 
-_partitions = {}  # (device, geometry CUs) -> (geometry stream, compute stream, raw handles)
+_partitions = {}  # (device, geometry CUs) -> (geometry, compute, tail streams, raw handles)
 
 
 @atexit.register
 def _destroy_partitions():
     """Release the CU-masked streams before the HIP runtime tears down (left to process exit,
     their destruction raced the runtime's own teardown under rocprofv3)."""
-    for key, (_, _, raw) in list(_partitions.items()):
+    for key, (*_, raw) in list(_partitions.items()):
         try:
             torch.cuda.synchronize(key[0])
         except Exception:
@@ -67,9 +80,7 @@ def _masked_stream(device, cus, ncu):
     return torch.cuda.ExternalStream(ptr.value, device=torch.device("cuda", device)), ptr.value
 
 
-def partition(device, geometry_cus):
-    """(geometry stream, compute stream) on `device`: `geometry_cus` CUs spread evenly over the
-    chip for the FPS chain, all the others for everything else.  Cached per (device, count)."""
+def _streams(device, geometry_cus):
     key = (device, geometry_cus)
     if key not in _partitions:
         ncu = _cu_count(device)
@@ -78,20 +89,43 @@ def partition(device, geometry_cus):
         geo = sorted({int(i * stride) for i in range(g)})
         rest = [c for c in range(ncu) if c not in set(geo)]
         (gs, gh), (cs, ch) = _masked_stream(device, geo, ncu), _masked_stream(device, rest, ncu)
-        _partitions[key] = (gs, cs, (gh, ch))
-    return _partitions[key][:2]
+        ts, th = _masked_stream(device, geo, ncu)
+        _partitions[key] = (gs, cs, ts, (gh, ch, th))
+    return _partitions[key][:3]
+
+
+def partition(device, geometry_cus):
+    """(geometry stream, compute stream) on `device`: `geometry_cus` CUs spread evenly over the
+    chip for the FPS chain, all the others for everything else.  Cached per (device, count)."""
+    return _streams(device, geometry_cus)[:2]
 
 
 class PipelinedForward:
     """``run(batches, extras=None)`` -> ``[model(x, *extra) for x, extra in ...]``, pipelined.
 
-    geometry_cus: CUs reserved for the FPS chain (default 32: one per cloud of a B=32 batch)."""
+    geometry_cus: CUs reserved for the FPS chain (default 32: one per cloud of a B=32 batch).
+    tail: run what follows the last SA layer (head, `post`) on the geometry CUs: False
+    (default), "auto" (when `run` gets no extras) or True."""
 
-    def __init__(self, model, geometry_cus=32):
+    def __init__(self, model, geometry_cus=32, tail=False):
         self.model = model
         self.geometry_cus = geometry_cus
+        self.tail = tail
         self.sas = [m for m in model.modules()
                     if isinstance(m, (PointNetSetAbstraction, PointNetSetAbstractionMsg))]
+
+    @staticmethod
+    def _to_tail(tail):
+        """Forward hook for the last SA module: hand its outputs to the tail stream and make it
+        current for the rest of the forward."""
+        def hook(module, inputs, output):
+            main = torch.cuda.current_stream()
+            tail.wait_stream(main)
+            for t in output if isinstance(output, (tuple, list)) else (output,):
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(tail)
+            torch.cuda.set_stream(tail)
+        return hook
 
     def _fps_chain(self, x):
         """FPS of every SA layer for input x ([B, C, N]); draws in layer order."""
@@ -109,16 +143,35 @@ class PipelinedForward:
     def run(self, batches, extras=None, post=None):
         """post(i, out) is called on the compute stream after batch i's forward (e.g. an
         all_gather of its logits)."""
+        return self._run_eager(batches, extras, post, self.tail)
+
+    def _run_eager(self, batches, extras, post, tail):
         if self.model.training:
             raise RuntimeError("pn2.pipeline: eval mode only")
         if not batches:
             return []
         dev = batches[0].device
-        geo, main = partition(dev.index, self.geometry_cus)
+        geo, main, tail = _streams(dev.index, self.geometry_cus)
         caller = torch.cuda.current_stream(dev)
         geo.wait_stream(caller)
         main.wait_stream(caller)
+        tail.wait_stream(caller)
         outs = []
+        handle = None
+        use_tail = (extras is None) if tail == "auto" else bool(tail)
+        if use_tail and self.sas:
+            handle = self.sas[-1].register_forward_hook(self._to_tail(tail))
+        try:
+            self._run(batches, extras, post, geo, main, outs)
+        finally:
+            if handle is not None:
+                handle.remove()
+        caller.wait_stream(main)
+        caller.wait_stream(geo)
+        caller.wait_stream(tail)
+        return outs
+
+    def _run(self, batches, extras, post, geo, main, outs):
         with torch.no_grad():
             with torch.cuda.stream(geo):
                 nxt = self._fps_chain(batches[0])
@@ -142,6 +195,175 @@ class PipelinedForward:
                     raise RuntimeError("pn2.pipeline: the model did not consume every "
                                        "precomputed FPS (SA layers called out of order?)")
                 outs.append(out)
-        caller.wait_stream(main)
-        caller.wait_stream(geo)
+
+
+def _clone(o):
+    if isinstance(o, torch.Tensor):
+        return o.clone()
+    if isinstance(o, (tuple, list)):
+        return type(o)(_clone(t) for t in o)
+    return o
+
+
+class _Slot:
+    """Static buffers and graphs of one pipeline slot (batches i with i % 2 == slot)."""
+
+
+class GraphedPipeline(PipelinedForward):
+    """``PipelinedForward`` with every stage replayed from HIP graphs: no per-kernel host work.
+
+    The eager pipeline issues ~25 launches plus the SA modules' Python per batch; on MI355X that
+    host time (~0.5 ms per SSG B=32 batch) is as long as the GPU work, so the GPU idles.  Here
+    each of two slots (batch i uses slot i % 2) holds static inputs and three captured graphs:
+      fps   the batch's FPS chain (``_fps_chain``), replayed on the geometry stream;
+      sa    the forward up to the last SA layer, replayed on the compute stream;
+      head  the rest of the forward, replayed on a third stream with the geometry CUs (``tail``;
+            with tail=False, head is part of sa).
+    The capture is split at the last SA layer by a forward hook (capture_end / capture_begin).
+    Events order the slot reuse: batch i+2's fps waits for batch i's sa (it overwrites the
+    slot's inputs and FPS outputs), batch i+2's sa waits for batch i's head (they share a memory
+    pool).  Static memory makes the tail safe for every head here, including the translation
+    heads' ``mean`` (see PipelinedForward).
+
+    RNG and results: as PipelinedForward.  The first batch of a new input signature (or after
+    any parameter change) runs through the eager pipeline -- its real result, its draws -- and
+    both slots are captured after it; the captures draw nothing.  Every replayed batch takes its
+    draws on the host in batch order (shard.draw_start, so shard.batch_shard applies) and uploads
+    them into the slot before its fps replay.  Outputs are cloned out of the static buffers on
+    the stream that produced them, so they stay valid.
+
+    Measured (SSG B=32 N=1024, untraced events, tools/debug/gpipe_events.py): host issue time
+    drops from ~470 to ~210 us per batch, but the compute stream stays the bound -- its graph
+    replay runs ~10% slower than the same kernels launched eagerly (gaps between graph nodes,
+    224 CUs) -- so today it gives 63.4k clouds/s (55.9k without the tail) against the eager
+    pipeline's 66.0k.  It is the launch to use once the compute stream's work drops below the
+    eager host issue time.
+    """
+
+    def __init__(self, model, geometry_cus=32, tail=True):
+        super().__init__(model, geometry_cus, bool(tail))
+        self._key = None
+        self._slots = None
+
+    def _state_key(self, x, extra):
+        from .graphs import _sig
+        ts = list(self.model.parameters()) + list(self.model.buffers())
+        return (_sig((x,) + tuple(extra)),) + tuple((t.data_ptr(), t._version) for t in ts)
+
+    def _capture(self, x, extra, dev, draws):
+        sl = _Slot()
+        sl.x = x.clone()
+        sl.extra = tuple(e.clone() for e in extra)
+        # the start slots exist before the capture: allocated inside it, a slot could share
+        # pool memory with a temporary the capture freed earlier, which the replay rewrites
+        # after the slot was uploaded
+        sl.starts = [(torch.empty(B, dtype=torch.long, device=dev), B, N) for B, N in draws]
+        it = iter(sl.starts)
+
+        def static_start(B, N, device):
+            t, b, n = next(it)
+            if (b, n) != (B, N):
+                raise RuntimeError("pn2.pipeline: FPS draw shapes changed during capture")
+            return t
+
+        sl.fps, sl.sa = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        sl.head = torch.cuda.CUDAGraph() if self.tail else None
+        fps_pool, fwd_pool = torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()
+
+        def split(module, inputs, output):
+            sl.sa.capture_end()
+            sl.sa_out = output
+            sl.head.capture_begin(pool=fwd_pool)
+
+        cs = torch.cuda.Stream(dev)
+        torch.cuda.synchronize(dev)
+        handle = self.sas[-1].register_forward_hook(split) if self.tail else None
+        try:
+            with torch.no_grad(), torch.cuda.stream(cs):
+                with shard.start_source(static_start):
+                    sl.fps.capture_begin(pool=fps_pool)
+                    sl.entries = self._fps_chain(sl.x)
+                    sl.fps.capture_end()
+                sl.sa.capture_begin(pool=fwd_pool)
+                with geometry.provide(dict(sl.entries)):
+                    sl.out = self.model(sl.x, *sl.extra)
+                (sl.head if self.tail else sl.sa).capture_end()
+        finally:
+            if handle is not None:
+                handle.remove()
+        torch.cuda.synchronize(dev)
+        return sl
+
+    def run(self, batches, extras=None, post=None):
+        if self.model.training:
+            raise RuntimeError("pn2.pipeline: eval mode only")
+        if not batches:
+            return []
+        extra_of = (lambda i: ()) if extras is None else (lambda i: tuple(extras[i]))
+        key = self._state_key(batches[0], extra_of(0))
+        if any(self._state_key(x, extra_of(i))[0] != key[0] for i, x in enumerate(batches)):
+            return self._run_eager(batches, extras, post, False)  # mixed shapes: eager
+        outs, first = [], 0
+        dev = batches[0].device
+        if key != self._key or self._slots is None:
+            self._slots = None
+            draws = []
+
+            def record(B, N, device):
+                draws.append((B, N))
+                return shard.draw_start(B, N).to(device, non_blocking=True)
+
+            with shard.start_source(record):
+                outs = self._run_eager(batches[:1], None if extras is None else extras[:1],
+                                       post, False)
+            self._slots = [self._capture(batches[0], extra_of(0), dev, draws) for _ in range(2)]
+            self._key = self._state_key(batches[0], extra_of(0))
+            first = 1
+        if first == len(batches):
+            return outs
+        geo, main, tail = _streams(dev.index, self.geometry_cus)
+        caller = torch.cuda.current_stream(dev)
+        for st in (geo, main, tail):
+            st.wait_stream(caller)
+        ev_fps, ev_sa, ev_head = [None, None], [None, None], [None, None]
+
+        def issue_fps(j):
+            s = j % 2
+            sl = self._slots[s]
+            with torch.cuda.stream(geo):
+                if ev_sa[s] is not None:  # batch j-2 is done with the slot's inputs
+                    geo.wait_event(ev_sa[s])
+                sl.x.copy_(batches[j], non_blocking=True)
+                for t, B, N in sl.starts:
+                    t.copy_(shard.draw_start(B, N), non_blocking=True)
+                sl.fps.replay()
+                ev_fps[s] = geo.record_event()
+
+        with torch.no_grad():
+            issue_fps(first)
+            for i in range(first, len(batches)):
+                s = i % 2
+                sl = self._slots[s]
+                if i + 1 < len(batches):
+                    issue_fps(i + 1)
+                with torch.cuda.stream(main):
+                    main.wait_event(ev_fps[s])
+                    if ev_head[s] is not None:  # batch i-2's head is done with the pool
+                        main.wait_event(ev_head[s])
+                    for d, e in zip(sl.extra, extra_of(i)):
+                        d.copy_(e, non_blocking=True)
+                    sl.sa.replay()
+                    ev_sa[s] = main.record_event()
+                ts = tail if sl.head is not None else main
+                with torch.cuda.stream(ts):
+                    if sl.head is not None:
+                        ts.wait_event(ev_sa[s])
+                        sl.head.replay()
+                    out = _clone(sl.out)
+                    if post is not None:
+                        out = post(i, out)
+                    ev_head[s] = ts.record_event()
+                outs.append(out)
+        for st in (geo, main, tail):
+            caller.wait_stream(st)
         return outs

@@ -270,8 +270,9 @@ def test_graph_replay_matches_eager(head):
     np.testing.assert_array_equal(rng_got.numpy(), rng_want.numpy())
 
 
-@pytest.mark.parametrize("head", ["ClsSSG", "ClsMSG", "TranslationSSG"])
-def test_pipelined_forward_matches_eager(head):
+@pytest.mark.parametrize("head,tail", [("ClsSSG", False), ("ClsSSG", "auto"), ("ClsMSG", False),
+                                       ("TranslationSSG", "auto")])
+def test_pipelined_forward_matches_eager(head, tail):
     """pn2.pipeline.PipelinedForward (FPS of batch i+1 on its own CUs while batch i runs) returns
     the eager forwards' results for a sequence of batches -- including a sharded call -- and
     leaves the CPU generator where the eager sequence leaves it.  Every SA output (the l3
@@ -305,7 +306,7 @@ def test_pipelined_forward_matches_eager(head):
     want_f, feats[:] = list(feats), []
     torch.manual_seed(31)
     with shard.batch_shard(2 * B, B):
-        got = [first(o) for o in PipelinedForward(model, geometry_cus=16).run(xs, extras)]
+        got = [first(o) for o in PipelinedForward(model, geometry_cus=16, tail=tail).run(xs, extras)]
     rng_got = torch.randint(0, 1 << 30, (4,))
     np.testing.assert_array_equal(rng_got.numpy(), rng_want.numpy())
     assert len(feats) == len(want_f) == len(xs)
@@ -313,3 +314,69 @@ def test_pipelined_forward_matches_eager(head):
         np.testing.assert_array_equal(g, w)
     for g, w in zip(got, want):
         np.testing.assert_allclose(g, w, rtol=1e-6, atol=1e-6 * float(np.abs(w).max()))
+
+
+@pytest.mark.parametrize("head,tail", [("ClsSSG", True), ("ClsSSG", False), ("ClsMSG", True),
+                                       ("TranslationSSG", True), ("RotationSSG", True)])
+def test_graphed_pipeline_matches_eager(head, tail):
+    """pn2.pipeline.GraphedPipeline (fps / SA / head replayed from HIP graphs on the geometry,
+    compute and tail streams, two slots) returns the eager forwards' results for a sequence of
+    batches -- the first batch eager, the rest replayed through both slots twice, under
+    shard.batch_shard -- and walks the CPU generator exactly as the eager sequence does.  The
+    cls heads return the last SA feature (l3f), held bit-identical; logits to 1e-6 relative
+    (the head's torch BLAS may pick another GEMM on a CU-restricted stream).  A second run()
+    replays without recapturing; an in-place BN change recaptures."""
+    from pn2 import heads as H
+    from pn2 import shard
+    from pn2.pipeline import GraphedPipeline
+    torch.manual_seed(8)
+    model = getattr(H, head)().eval()
+    cases.randomize_bn(model, 8)
+    model = model.to(DEV)
+    kind = "onehot10" if head in ("TranslationSSG", "RotationSSG") else "uniform3"
+    B, N = (8, 2048) if head == "ClsMSG" else (16, 1024)
+    xs = [cases.cloud(kind, B, N, 90 + i).permute(0, 2, 1).contiguous().to(DEV) for i in range(6)]
+    extras = None
+    if head.startswith("Translation"):
+        extras = [(torch.randn(B, 3, generator=torch.Generator().manual_seed(i)).to(DEV),)
+                  for i in range(6)]
+
+    def as_np(o):
+        return [t.cpu().numpy() for t in (o if isinstance(o, tuple) else (o,))
+                if isinstance(t, torch.Tensor)]
+
+    torch.manual_seed(31)
+    with torch.no_grad(), shard.batch_shard(2 * B, B):
+        want = [as_np(model(x, *(extras[i] if extras else ()))) for i, x in enumerate(xs)]
+    rng_want = torch.randint(0, 1 << 30, (4,))
+
+    gp = GraphedPipeline(model, geometry_cus=16, tail=tail)
+    torch.manual_seed(31)
+    with shard.batch_shard(2 * B, B):
+        got = [as_np(o) for o in gp.run(xs[:3], extras[:3] if extras else None)]
+        slots = gp._slots
+        got += [as_np(o) for o in gp.run(xs[3:], extras[3:] if extras else None)]
+        assert gp._slots is slots  # replayed, not recaptured
+    rng_got = torch.randint(0, 1 << 30, (4,))
+    np.testing.assert_array_equal(rng_got.numpy(), rng_want.numpy())
+    assert len(got) == len(want)
+    if head.startswith("Cls"):  # l3f: the SA path, bit-exact
+        for i, (g, w) in enumerate(zip(got, want)):
+            np.testing.assert_array_equal(g[1], w[1], err_msg="l3f of batch %d" % i)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert len(g) == len(w)
+        for k, (a, b) in enumerate(zip(g, w)):
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * float(np.abs(b).max()),
+                                       err_msg="output %d of batch %d" % (k, i))
+
+    # a parameter change recaptures and still matches eager
+    next(b for n, b in model.sa1.named_buffers() if n.endswith("running_mean")).add_(0.25)
+    torch.manual_seed(5)
+    with torch.no_grad():
+        want2 = [as_np(model(x, *(extras[i] if extras else ()))) for i, x in enumerate(xs[:3])]
+    torch.manual_seed(5)
+    got2 = [as_np(o) for o in gp.run(xs[:3], extras[:3] if extras else None)]
+    assert gp._slots is not slots
+    for g, w in zip(got2, want2):
+        for a, b in zip(g, w):
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * float(np.abs(b).max()))
