@@ -6,10 +6,12 @@ of N=1024 points per GPU, on the MI355X-native SA path.
 
 One step = one forward of the head over every rank's batch shard (weak scaling: B clouds per
 GPU, global batch = B*N) followed by the RCCL all_gather of the logits -- the only exchange the
-data-parallel path has.  Single-head configs run the K steps through pn2.pipeline (the FPS
-chain of step i+1 on a few dedicated CUs while step i's ball queries, MLPs and head run on the
-others; every step computes exactly the eager forward, with the same CPU-RNG draws);
---no-pipeline runs them one after the other, --graph replays each as a HIP graph.  Inputs are
+data-parallel path has.  Single-head configs run the K steps through
+pn2.pipeline.GraphedPipeline (the FPS chain of step i+1 on its own stream while step i's ball
+queries and MLPs run, the head on a third stream, every stage replayed from HIP graphs; every
+step computes exactly the eager forward, with the same CPU-RNG draws); --eager-pipeline issues
+the same pipeline op by op, --no-pipeline runs the steps one after the other, --graph replays
+each as one HIP graph.  Inputs are
 resident in HBM before the timed region, which carries no instrumentation.  Rank 0 prints one
 JSON line (contract in the task statement) with:
   value         clouds/s of the timed region; eager_value is the same K steps run one after
@@ -66,17 +68,17 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline sample")
     ap.add_argument("--no-kernel-timer", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the forward as a HIP graph")
-    ap.add_argument("--graph-pipeline", action="store_true",
-                    help="pipelined launch with every stage replayed from HIP graphs "
-                         "(pn2.pipeline.GraphedPipeline)")
+    ap.add_argument("--eager-pipeline", action="store_true",
+                    help="pipelined launch issued op by op (pn2.pipeline.PipelinedForward) "
+                         "instead of replayed from HIP graphs (GraphedPipeline, the default)")
     ap.add_argument("--tail", action="store_true",
-                    help="eager pipelined: run the head on the geometry CUs after the last SA "
-                         "layer (see pn2.pipeline; default off)")
+                    help="eager pipeline: run the head on its own stream (default off there)")
     ap.add_argument("--no-tail", action="store_true",
-                    help="graph pipelined: keep the head on the compute stream")
+                    help="graphed pipeline: keep the head on the compute stream")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="plain eager steps (default for single-head configs: pn2.pipeline)")
-    ap.add_argument("--geometry-cus", type=int, default=32, help="CUs reserved for the FPS chain")
+    ap.add_argument("--geometry-cus", type=int, default=0,
+                    help="CUs reserved for the FPS chain (0: streams share every CU)")
     return ap.parse_args()
 
 
@@ -193,7 +195,7 @@ def main():
     pf = None
     if pipelined:
         from pn2.pipeline import GraphedPipeline, PipelinedForward
-        if a.graph_pipeline:
+        if not a.eager_pipeline:
             pf = GraphedPipeline(eager_models[0], geometry_cus=a.geometry_cus,
                                  tail=not a.no_tail)
         else:
@@ -286,11 +288,12 @@ def main():
                        "parallelism": "dp%d" % world},
             "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
             "launch": ("hip_graph" if a.graph else
-                       "%spipelined(fps%s on %d CUs)" % (
-                           "graphed " if a.graph_pipeline else "",
-                           " + head" if (a.graph_pipeline and not a.no_tail) or (
+                       "%s pipeline (fps%s stream%s)" % (
+                           "eager" if a.eager_pipeline else "graphed",
+                           " + head" if (not a.eager_pipeline and not a.no_tail) or (
                                a.tail and not names[0].startswith("translation")) else "",
-                           a.geometry_cus)
+                           " on %d dedicated CUs" % a.geometry_cus if a.geometry_cus > 0
+                           else "s sharing all CUs")
                        if pipelined else "eager"),
             "eager_value": round(eager_value, 2),
         }

@@ -58,7 +58,7 @@ struct ChainArgs {
     float *out;
     int64_t ostride;
     int lds_bn;    // byte offset of the staged BN scale/shift
-    int lds_ring;  // byte offset of the per-wave weight rings
+    int lds_ring;  // byte offset of the workgroup weight ring (kStages stage buffers)
 };
 
 __device__ __forceinline__ Split load_w(const ChainLayer &L, int t, int kb, int lane) {
@@ -93,12 +93,23 @@ __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const floa
 }
 
 
-// ---- per-wave weight ring (layers 1 and 2).  A step = one (tile, k-block) of a layer = its
-// three 1 KB plane fragments, copied HBM/L2 -> LDS by global_load_lds (lane-linear, no VGPRs)
-// R-1 steps ahead of use into this wave's own ring of R slots: no cross-wave barrier, and the
-// only vector-memory traffic in flight is the ring (BN parameters are staged in LDS), so a
-// counted s_waitcnt vmcnt retires exactly the step about to be read.
+// ---- workgroup weight ring.  A step = one (tile, k-block) of a layer = its three 1 KB plane
+// fragments; every wave of the workgroup consumes the same steps in the same order (its own 32
+// rows), so one LDS copy of a step feeds all four waves' MFMAs (128 rows per 3 KB of weights --
+// per-wave copies made the L2 -> LDS weight stream, not the MFMA, the bound).  Steps are copied
+// HBM/L2 -> LDS by global_load_lds (lane-linear, no VGPRs) in stages of kChainWaves steps: wave
+// w copies step kChainWaves*st + w of stage st into stage buffer st % kStages.  At the first
+// step of stage st every wave
+//   1. waits for its own earlier LDS reads (lgkmcnt(0): stage st-1 is no longer read by it),
+//   2. waits for its own copy of stage st (counted vmcnt: stages st+1 .. st+kStages-2 stay in
+//      flight),
+//   3. s_barrier (raw: __syncthreads' fence would wait vmcnt(0) and drain the ring) -- now
+//      stage st is whole in LDS and no wave reads stage st-1 any more,
+//   4. copies its step of stage st+kStages-1 into stage st-1's buffer.
+// Past the last step the copies repeat the last step (same counts, never read).
 constexpr int kStepBytes = 3 * 1024;
+constexpr int kStages = 3;
+constexpr int kStageBytes = kChainWaves * kStepBytes;
 
 // frag: the step's plane-0 fragment (wave-uniform); loff = lane * 16 -- the uniform-base +
 // lane-offset form lets the copy use a scalar base address (no per-copy vector address math)
@@ -110,25 +121,22 @@ __device__ __forceinline__ void ring_issue(const bf16x8 *frag, int64_t plane, ch
                                          (lds_void *)(slot + p * 1024), 16, 0, 0);
 }
 
-
-
-// Step j refills the slot of step j-1 before waiting for its own copies, so NR-1 later steps
-// are in flight at every wait (issues past the end repeat the last step into an
-// already-consumed slot): one constant count retires step j; stores issued meanwhile only
-// make the count conservative.
-template <int NR>
-__device__ __forceinline__ void ring_wait() {
-    if constexpr (NR == 4) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else if constexpr (NR == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// step 2 above: this wave's copies of the kStages-2 younger stages may stay in flight
+__device__ __forceinline__ void stage_wait() {
+    static_assert(kStages == 3, "stage_wait count");
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
 }
 
-// Before a slot is refilled, the previous step's fragment reads from it must have returned.
-// The compiler does not see that global_load_lds (addressed through M0) writes that slot, so
-// the memory clobber also keeps those reads from being scheduled after the refill.
+// Before a buffer is refilled, this wave's reads of it must have returned.  The compiler does
+// not see that global_load_lds (addressed through M0) writes that buffer, so the memory clobber
+// also keeps those reads from being scheduled after the refill.
 __device__ __forceinline__ void ring_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-
+__device__ __forceinline__ void stage_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 
 // KB0M > 0: the layer-0 input (<= KB0M k-blocks) is gathered once into registers and layer 0 runs
 // tile by tile from the ring like layers 1 and 2; KB0M == 0: layer 0 streams its input blocks
@@ -137,7 +145,6 @@ template <int T0, int T1, int KB0M>
 __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_eu(2))) void sa_chain_kernel(
     const ChainArgs A) {
     extern __shared__ __attribute__((aligned(16))) char csm[];
-    constexpr int NR = (T0 * T1 >= 8) ? 4 : 3;  // ring slots
     constexpr int KB1 = 2 * T0, KB2 = 2 * T1;
     unsigned *cpool = reinterpret_cast<unsigned *>(csm);
     const int tid = threadIdx.x;
@@ -160,35 +167,43 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     if (A.pool_mode == 1)
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
     __syncthreads();
-    char *ring = csm + A.lds_ring + wave * (NR * kStepBytes);
+    char *ring = csm + A.lds_ring;
     const unsigned loff = (unsigned)lane * 16u;
-    // Ring steps in consumption order: layers 0 (resident input) and 1 block-major, layer 2
-    // tile-major.  Step j first refills the previous step's slot with step j+NR-1 (after
-    // ring_fence), then waits for and reads its own; source addresses come from scalar
-    // arithmetic on the layer's base (compile-time inside the unrolled loops), and past the end
-    // the last step repeats into an already-consumed slot.
-    int nissued = 0, nread = 0;
-    auto issue_l = [&](const ChainLayer &L, int t, int kb) {
-        ring_issue(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64,
-                   ring + (nissued % NR) * kStepBytes, loff);
-        ++nissued;
+    // Ring steps in consumption order: layers 0 (resident input only) and 1 block-major, layer 2
+    // tile-major; source addresses come from scalar arithmetic on the layer's base.
+    auto issue_l = [&](const ChainLayer &L, int t, int kb, char *dst) {
+        ring_issue(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64, dst, loff);
     };
-    auto issue2 = [&](int z) {  // layer-2 step z
+    auto issue2 = [&](int z, char *dst) {  // layer-2 step z
         z = min(z, L2.tiles * KB2 - 1);
-        issue_l(L2, z / KB2, z % KB2);
+        issue_l(L2, z / KB2, z % KB2, dst);
     };
-    auto issue1 = [&](int y) {  // layer-1 step y (block-major)
-        if (y < T1 * KB1) issue_l(L1, y % T1, y / T1);
-        else issue2(y - T1 * KB1);
+    auto issue1 = [&](int y, char *dst) {  // layer-1 step y (block-major)
+        if (y < T1 * KB1) issue_l(L1, y % T1, y / T1, dst);
+        else issue2(y - T1 * KB1, dst);
     };
     const int n0 = T0 * L0.kb;
-    auto issue0 = [&](int x) {  // layer-0 step x (block-major)
-        if (x < n0) issue_l(L0, x % T0, x / T0);
-        else issue1(x - n0);
+    auto issue_stage = [&](int st) {  // this wave's step of stage st
+        const int x = st * kChainWaves + wave;
+        char *dst = ring + (st % kStages) * kStageBytes + wave * kStepBytes;
+        if constexpr (KB0M > 0) {
+            if (x < n0) issue_l(L0, x % T0, x / T0, dst);
+            else issue1(x - n0, dst);
+        } else {
+            issue1(x, dst);
+        }
     };
+    int nread = 0;
     auto read_w = [&]() {
-        ring_wait<NR>();
-        const Split w = ring_read(ring + (nread % NR) * kStepBytes, lane);
+        if ((nread & (kChainWaves - 1)) == 0) {  // first step of a stage
+            const int st = nread / kChainWaves;
+            ring_fence();
+            stage_wait();
+            stage_barrier();
+            issue_stage(st + kStages - 1);
+        }
+        const Split w = ring_read(ring + ((nread / kChainWaves) % kStages) * kStageBytes +
+                                      (nread & (kChainWaves - 1)) * kStepBytes, lane);
         ++nread;
         return w;
     };
@@ -245,7 +260,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             }
         }
 #pragma unroll
-        for (int j = 0; j < NR - 1; ++j) issue0(j);  // overlaps the gather's latency
+        for (int st = 0; st < kStages - 1; ++st) issue_stage(st);  // overlaps the gather's latency
         cfloatx16 acc[T0];
 #pragma unroll
         for (int t = 0; t < T0; ++t)
@@ -256,11 +271,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             if (kb < L0.kb) {
                 const Split xs = split8(x[kb]);
 #pragma unroll
-                for (int t = 0; t < T0; ++t) {
-                    ring_fence();
-                    issue0(kb * T0 + t + NR - 1);
-                    acc[t] = mma6_wa(read_w(), xs, acc[t]);
-                }
+                for (int t = 0; t < T0; ++t) acc[t] = mma6_wa(read_w(), xs, acc[t]);
             }
         }
 #pragma unroll
@@ -285,7 +296,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
         // layer 0's loads are all consumed: start the ring, then the epilogue hides its latency
 #pragma unroll
-        for (int j = 0; j < NR - 1; ++j) issue1(j);
+        for (int st = 0; st < kStages - 1; ++st) issue_stage(st);
 #pragma unroll
         for (int t = 0; t < T0; ++t) hidden_epilogue(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
     }
@@ -302,11 +313,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int kb = 0; kb < KB1; ++kb)
 #pragma unroll
-            for (int t = 0; t < T1; ++t) {
-                ring_fence();
-                issue1(kb * T1 + t + NR - 1);
-                acc[t] = mma6_wa(read_w(), X1[kb], acc[t]);
-            }
+            for (int t = 0; t < T1; ++t) acc[t] = mma6_wa(read_w(), X1[kb], acc[t]);
 #pragma unroll
         for (int t = 0; t < T1; ++t) hidden_epilogue(acc[t], al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
     }
@@ -318,11 +325,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < KB2; ++kb) {
-            ring_fence();
-            issue2(t * KB2 + kb + NR - 1);
-            acc = mma6_wb(X2[kb], read_w(), acc);
-        }
+        for (int kb = 0; kb < KB2; ++kb) acc = mma6_wb(X2[kb], read_w(), acc);
         // max over rows of relu(fma(acc, al, be)) = relu(fma(extreme, al, be)) exactly: fma with
         // a fixed al is monotone in acc (non-decreasing for al >= 0, else non-increasing) and
         // so is relu -- only the row max (al >= 0) or min of the accumulator is needed.
@@ -545,8 +548,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     A.lds_bn = (int)((lds + 15) / 16 * 16);
     const size_t bn_bytes = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + coutL);
     A.lds_ring = (int)((A.lds_bn + bn_bytes + 15) / 16 * 16);
-    const int ring_slots = (T0 * T1 >= 8) ? 4 : 3;  // = NR of sa_chain_kernel
-    lds = (size_t)A.lds_ring + (size_t)kChainWaves * ring_slots * kStepBytes;
+    lds = (size_t)A.lds_ring + (size_t)kStages * kStageBytes;
     int rc = PN2_EUNSUPPORTED;
 #define PN2_CHAIN_GO(a, b, c) \
     if (T0 == a && T1 == b && KB0M == c) rc = launch_chain_sig<a, b, c>(A, grid, lds, st);

@@ -1,31 +1,38 @@
-"""Pipelined eval forward over a stream of batches, with the GPU partitioned by CUs.
+"""Pipelined eval forward over a stream of batches.
 
 Every SA layer's farthest point sampling depends only on the point coordinates (sa1 samples the
 input cloud, sa2 the centroids sa1 chose, ...), never on an MLP output, so a batch's whole FPS
-chain can run before its forward.  ``PipelinedForward`` runs the FPS chain of batch i+1 while
-the ball queries, MLPs and head of batch i run, on two HIP streams that own disjoint CU sets
-(hipExtStreamCreateWithCUMask through pn2_stream_create_cu_masked): FPS is a serial,
-latency-bound loop of one workgroup per cloud, so it gets a few dedicated CUs instead of
-time-sharing CUs with MFMA work (which slows its loop ~2.7x, measured), and the MFMA kernels
-keep the rest of the chip.
+chain can run before its forward.  The pipeline runs the FPS chain of batch i+1 on a
+*geometry* stream while the ball queries and MLPs of batch i run on a *compute* stream: FPS is a
+serial, latency-bound loop of one workgroup per cloud (32 workgroups at B=32) that leaves
+almost all of the chip idle, so overlapping it takes it off the critical path.
+
+``GraphedPipeline`` (the launch bench.py uses) replays every stage from HIP graphs; the eager
+``PipelinedForward`` issues ~25 launches per batch from Python, ~470 us of host time at SSG
+B=32, which is longer than the compute stream's work once the MLP kernels are fast.
+
+CUs.  By default (geometry_cus=0) the streams are ordinary streams sharing every CU, geometry
+at high priority.  ``geometry_cus > 0`` gives the geometry stream its own CUs instead
+(hipExtStreamCreateWithCUMask through pn2_stream_create_cu_masked; see ``_streams`` for how
+MI355X maps mask bits to XCDs).  Measured, SSG B=32 N=1024, graphed: shared 69.5k / 69.9k
+clouds/s; 8 dedicated CUs (1 per XCD) 65.0k / 65.1k; 24 CUs 63.3k / 64.4k -- FPS co-resident
+with the MFMA kernels costs the chains less than the CUs a partition withholds from them.
 
 The tail of each forward -- everything after the last SA layer returns (the FC head, `post`) --
-runs on a third stream with the geometry CUs: it is a dozen tiny launches (the head's largest
-GEMM has 2 workgroups) that would otherwise sit on the compute stream between batch i's last
-MLP and batch i+1's first, while the geometry CUs have room (FPS is ~45% of a step).  The switch
-is a forward hook on the last SA module, active only inside ``run``.  The last SA layer's
-outputs are handed over with ``record_stream``; any other compute-stream tensor the tail reads
-(e.g. the translation heads' ``mean``, computed before sa1 and added after the head) would not
-be, so ``tail="auto"`` uses it only for models called without extra inputs (every reference
-head but translation_*); ``tail=True`` forces it.  Off by default: with eager launches the host
-issue time per batch (~470 us at SSG B=32, measured) is as long as the compute stream's work,
-and the extra stream hops cost more than the tail frees (62.6k vs 66.0k clouds/s).  It pays in
-``GraphedPipeline`` (default on there).
+can run on a third stream: it is a dozen tiny launches (the head's largest GEMM has 2
+workgroups) that would otherwise sit on the compute stream between batch i's last MLP and batch
+i+1's first.  The switch is a forward hook on the last SA module, active only inside ``run``.
+The last SA layer's outputs are handed over with ``record_stream``; any other compute-stream
+tensor the tail reads (e.g. the translation heads' ``mean``, computed before sa1 and added
+after the head) would not be, so ``tail="auto"`` uses it only for models called without extra
+inputs (every reference head but translation_*); ``tail=True`` forces it.  Off by default in
+the eager pipeline (its host issue time is the bound there: 62.6k vs 66.0k clouds/s measured),
+on in ``GraphedPipeline``, whose static buffers make it safe for every head.
 
 Results and RNG.  Every batch computes what ``model(x)`` computes: the SA layers run the same
 kernels and produce the same bits (test_pipelined_forward_matches_eager); the head's own
-``nn.Linear`` layers go through torch's BLAS, which may choose a different GEMM kernel on the
-CU-restricted stream (last-ulp differences in logits).  The reference draws one ``torch.randint(0, N, (B,))`` per SA layer from the CPU
+``nn.Linear`` layers go through torch's BLAS, which may choose a different GEMM kernel on
+another stream (last-ulp differences in logits).  The reference draws one ``torch.randint(0, N, (B,))`` per SA layer from the CPU
 generator (pointnet2_utils.py:59); here batch i's draws (all its layers, in layer order) are
 taken before batch i+1's -- the order a sequence of eager forwards takes them -- so
 ``run(batches)`` matches ``[model(x) for x in batches]`` and leaves the generator in the same
@@ -80,14 +87,28 @@ def _masked_stream(device, cus, ncu):
     return torch.cuda.ExternalStream(ptr.value, device=torch.device("cuda", device)), ptr.value
 
 
+# hipExtStreamCreateWithCUMask on MI355X (measured, tools/micro/cu_mask_map.hip): mask bit i
+# belongs to XCD i % 8 and selects CU i / 8 of it, and an XCD whose share of the mask is empty
+# is NOT restricted (all 32 of its CUs run the stream).  So a partition is a contiguous block of
+# bits: [0, g) = g/8 CUs on every XCD, [g, 256) = the other CUs of every XCD.  (A mask spread
+# with stride 8 -- bits 0, 8, 16, ... -- is XCD 0 alone plus the seven unrestricted XCDs: the
+# whole chip.)
+_XCDS = 8
+
+
 def _streams(device, geometry_cus):
     key = (device, geometry_cus)
+    if key not in _partitions and int(geometry_cus) <= 0:
+        # no partition: three ordinary streams sharing every CU, geometry at high priority
+        dev = torch.device("cuda", device)
+        lo, hi = torch.cuda.Stream.priority_range()
+        _partitions[key] = (torch.cuda.Stream(dev, priority=min(lo, hi)), torch.cuda.Stream(dev),
+                            torch.cuda.Stream(dev), ())
     if key not in _partitions:
         ncu = _cu_count(device)
-        g = max(1, min(int(geometry_cus), ncu - 1))
-        stride = ncu / g
-        geo = sorted({int(i * stride) for i in range(g)})
-        rest = [c for c in range(ncu) if c not in set(geo)]
+        per = max(1, min(int(geometry_cus) // _XCDS, ncu // _XCDS - 1))  # CUs per XCD
+        geo = list(range(per * _XCDS))
+        rest = list(range(per * _XCDS, ncu))
         (gs, gh), (cs, ch) = _masked_stream(device, geo, ncu), _masked_stream(device, rest, ncu)
         ts, th = _masked_stream(device, geo, ncu)
         _partitions[key] = (gs, cs, ts, (gh, ch, th))
@@ -95,19 +116,20 @@ def _streams(device, geometry_cus):
 
 
 def partition(device, geometry_cus):
-    """(geometry stream, compute stream) on `device`: `geometry_cus` CUs spread evenly over the
-    chip for the FPS chain, all the others for everything else.  Cached per (device, count)."""
+    """(geometry stream, compute stream) on `device`: `geometry_cus` CUs (rounded down to a
+    multiple of the XCD count, at least one per XCD) for the FPS chain, all the others for
+    everything else.  Cached per (device, count)."""
     return _streams(device, geometry_cus)[:2]
 
 
 class PipelinedForward:
     """``run(batches, extras=None)`` -> ``[model(x, *extra) for x, extra in ...]``, pipelined.
 
-    geometry_cus: CUs reserved for the FPS chain (default 32: one per cloud of a B=32 batch).
+    geometry_cus: 0 (default): streams share every CU; > 0: CUs reserved for the FPS chain.
     tail: run what follows the last SA layer (head, `post`) on the geometry CUs: False
     (default), "auto" (when `run` gets no extras) or True."""
 
-    def __init__(self, model, geometry_cus=32, tail=False):
+    def __init__(self, model, geometry_cus=0, tail=False):
         self.model = model
         self.geometry_cus = geometry_cus
         self.tail = tail
@@ -205,6 +227,11 @@ def _clone(o):
     return o
 
 
+# thread-local capture: other threads (the RCCL watchdog of a multi-GPU run) may keep querying
+# their own events while a pipeline slot is captured
+_MODE = "thread_local"
+
+
 class _Slot:
     """Static buffers and graphs of one pipeline slot (batches i with i % 2 == slot)."""
 
@@ -232,15 +259,13 @@ class GraphedPipeline(PipelinedForward):
     them into the slot before its fps replay.  Outputs are cloned out of the static buffers on
     the stream that produced them, so they stay valid.
 
-    Measured (SSG B=32 N=1024, untraced events, tools/debug/gpipe_events.py): host issue time
-    drops from ~470 to ~210 us per batch, but the compute stream stays the bound -- its graph
-    replay runs ~10% slower than the same kernels launched eagerly (gaps between graph nodes,
-    224 CUs) -- so today it gives 63.4k clouds/s (55.9k without the tail) against the eager
-    pipeline's 66.0k.  It is the launch to use once the compute stream's work drops below the
-    eager host issue time.
+    Measured (SSG B=32 N=1024, shared CUs): 69.5k-69.9k clouds/s, against 52.5k-67.6k for the
+    eager pipeline (host-bound: ~470 us of issue per batch vs ~210 us here,
+    tools/debug/host_cost.py).  Without the tail the head's dozen launches sit on the compute
+    stream (59.5k).
     """
 
-    def __init__(self, model, geometry_cus=32, tail=True):
+    def __init__(self, model, geometry_cus=0, tail=True):
         super().__init__(model, geometry_cus, bool(tail))
         self._key = None
         self._slots = None
@@ -273,7 +298,7 @@ class GraphedPipeline(PipelinedForward):
         def split(module, inputs, output):
             sl.sa.capture_end()
             sl.sa_out = output
-            sl.head.capture_begin(pool=fwd_pool)
+            sl.head.capture_begin(pool=fwd_pool, capture_error_mode=_MODE)
 
         cs = torch.cuda.Stream(dev)
         torch.cuda.synchronize(dev)
@@ -281,10 +306,10 @@ class GraphedPipeline(PipelinedForward):
         try:
             with torch.no_grad(), torch.cuda.stream(cs):
                 with shard.start_source(static_start):
-                    sl.fps.capture_begin(pool=fps_pool)
+                    sl.fps.capture_begin(pool=fps_pool, capture_error_mode=_MODE)
                     sl.entries = self._fps_chain(sl.x)
                     sl.fps.capture_end()
-                sl.sa.capture_begin(pool=fwd_pool)
+                sl.sa.capture_begin(pool=fwd_pool, capture_error_mode=_MODE)
                 with geometry.provide(dict(sl.entries)):
                     sl.out = self.model(sl.x, *sl.extra)
                 (sl.head if self.tail else sl.sa).capture_end()

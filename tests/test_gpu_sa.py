@@ -350,7 +350,7 @@ def test_graphed_pipeline_matches_eager(head, tail):
         want = [as_np(model(x, *(extras[i] if extras else ()))) for i, x in enumerate(xs)]
     rng_want = torch.randint(0, 1 << 30, (4,))
 
-    gp = GraphedPipeline(model, geometry_cus=16, tail=tail)
+    gp = GraphedPipeline(model, geometry_cus=0 if tail else 16, tail=tail)
     torch.manual_seed(31)
     with shard.batch_shard(2 * B, B):
         got = [as_np(o) for o in gp.run(xs[:3], extras[:3] if extras else None)]
