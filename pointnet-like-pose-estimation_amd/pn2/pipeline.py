@@ -282,7 +282,12 @@ class GraphedPipeline(PipelinedForward):
         # the start slots exist before the capture: allocated inside it, a slot could share
         # pool memory with a temporary the capture freed earlier, which the replay rewrites
         # after the slot was uploaded
-        sl.starts = [(torch.empty(B, dtype=torch.long, device=dev), B, N) for B, N in draws]
+        # all of a batch's start draws in one device buffer: one upload per batch
+        sl.start_buf = torch.empty(sum(B for B, _ in draws), dtype=torch.long, device=dev)
+        sl.starts, off = [], 0
+        for B, N in draws:
+            sl.starts.append((sl.start_buf[off:off + B], B, N))
+            off += B
         it = iter(sl.starts)
 
         def static_start(B, N, device):
@@ -351,6 +356,7 @@ class GraphedPipeline(PipelinedForward):
         for st in (geo, main, tail):
             st.wait_stream(caller)
         ev_fps, ev_sa, ev_head = [None, None], [None, None], [None, None]
+        starts = self._draw_all(len(batches) - first)
 
         def issue_fps(j):
             s = j % 2
@@ -359,8 +365,7 @@ class GraphedPipeline(PipelinedForward):
                 if ev_sa[s] is not None:  # batch j-2 is done with the slot's inputs
                     geo.wait_event(ev_sa[s])
                 sl.x.copy_(batches[j], non_blocking=True)
-                for t, B, N in sl.starts:
-                    t.copy_(shard.draw_start(B, N), non_blocking=True)
+                sl.start_buf.copy_(starts[j - first], non_blocking=True)
                 sl.fps.replay()
                 ev_fps[s] = geo.record_event()
 
@@ -389,6 +394,30 @@ class GraphedPipeline(PipelinedForward):
                         out = post(i, out)
                     ev_head[s] = ts.record_event()
                 outs.append(out)
+        self._pinned_evs[self._pinned_cur] = geo.record_event()  # uploads read it
         for st in (geo, main, tail):
             caller.wait_stream(st)
         return outs
+
+    def _draw_all(self, k):
+        """Start draws of the next k batches, taken now in batch order then layer order (the
+        order k eager forwards take them), into rows of a pinned host buffer: one asynchronous
+        upload per batch, no per-draw pinning (hipHostMalloc) on the issue path.  Two buffers
+        alternate across calls; one is refilled once the uploads of the call before last ran."""
+        shapes = [(B, N) for _, B, N in self._slots[0].starts]
+        width = sum(B for B, _ in shapes)
+        if not hasattr(self, "_pinned"):
+            self._pinned, self._pinned_evs, self._pinned_cur = [None, None], [None, None], 0
+        c = self._pinned_cur = 1 - self._pinned_cur
+        if self._pinned_evs[c] is not None:
+            self._pinned_evs[c].synchronize()
+        buf = self._pinned[c]
+        if buf is None or buf.shape[0] < k or buf.shape[1] != width:
+            buf = self._pinned[c] = torch.empty(max(k, 64), width, dtype=torch.long,
+                                                pin_memory=True)
+        for j in range(k):
+            off = 0
+            for B, N in shapes:
+                buf[j, off:off + B] = shard.draw_start(B, N, pin=False)
+                off += B
+        return buf

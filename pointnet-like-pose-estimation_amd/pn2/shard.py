@@ -33,9 +33,9 @@ def batch_shard(global_batch, offset):
         _state.spec = prev
 
 
-def draw_start(B, N):
-    """CPU int64 [B]: the reference's randint draw (or this shard's slice of it), pinned so the
-    host->device copy is asynchronous."""
+def draw_start(B, N, pin=True):
+    """CPU int64 [B]: the reference's randint draw (or this shard's slice of it), pinned (unless
+    pin=False) so the host->device copy is asynchronous."""
     spec = getattr(_state, "spec", None)
     if spec is None:
         t = torch.randint(0, N, (B,), dtype=torch.long)
@@ -44,7 +44,7 @@ def draw_start(B, N):
         if off + B > gb:
             raise ValueError("batch_shard: shard [%d, %d) outside global batch %d" % (off, off + B, gb))
         t = torch.randint(0, N, (gb,), dtype=torch.long)[off:off + B]
-    return t.pin_memory() if torch.cuda.is_available() else t
+    return t.pin_memory() if pin and torch.cuda.is_available() else t
 
 
 def device_start(B, N, device):

@@ -20,7 +20,7 @@ cases.randomize_bn(model, 8)
 model = model.to(DEV)
 B, N = 32, 1024
 x = cases.cloud("uniform3", B, N, 90).permute(0, 2, 1).contiguous().to(DEV)
-gp = GraphedPipeline(model, geometry_cus=32, tail=True)
+gp = GraphedPipeline(model, geometry_cus=int(os.environ.get("GEO_CUS", "0")), tail=True)
 gp.run([x] * 3)
 torch.cuda.synchronize()
 sl = gp._slots[0]
@@ -40,6 +40,7 @@ def t_host(fn, n=50):
 for name, fn in [
     ("draw_start (cpu randint)", lambda: shard.draw_start(B, N)),
     ("start upload copy_", lambda: sl.starts[0][0].copy_(shard.draw_start(B, N), non_blocking=True)),
+    ("pre-drawn upload", lambda: sl.start_buf.copy_(gp._pinned[gp._pinned_cur][0], non_blocking=True)),
     ("x copy_ (d2d)", lambda: sl.x.copy_(x, non_blocking=True)),
     ("fps graph replay", lambda: sl.fps.replay()),
     ("sa graph replay", lambda: sl.sa.replay()),
@@ -52,7 +53,7 @@ for name, fn in [
         h, w = t_host(fn, 20 if "eager" in name else 50)
     print("%-28s host %8.1f us/call   wall %8.1f us/call" % (name, h, w))
 
-for k in (10, 40):
+for k in (10, 40, 100):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     gp.run([x] * k)
@@ -62,7 +63,7 @@ for k in (10, 40):
     print("GraphedPipeline.run(%d): host %.1f us/batch, wall %.1f us/batch" % (k, (t1 - t0) / k * 1e6, (t2 - t0) / k * 1e6))
 pf = PipelinedForward(model, geometry_cus=32)
 pf.run([x] * 3)
-for k in (10, 40):
+for k in (10, 40, 100):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     pf.run([x] * k)
