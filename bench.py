@@ -45,7 +45,8 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "point-clouds/sec forward, SSG B=32 N=1024, at 1/2/4/8 MI355X"
 PEAK_F32_MFMA = 157.3  # TFLOP/s, MI355X_MICROARCH.md chip-level table (dense fp32 MFMA)
-PEAK_SPLIT = 16 * PEAK_F32_MFMA / 6  # fp32-equivalent ceiling of 6-product split-bf16 MFMA
+PEAK_BF16_MFMA = 16 * PEAK_F32_MFMA  # TFLOP/s, dense bf16 MFMA (2516.8)
+PEAK_SPLIT = PEAK_BF16_MFMA / 6  # fp32-equivalent ceiling of 6-product split-bf16 MFMA
 PEAK_HBM = 8000.0      # GB/s
 
 CONFIGS = {
@@ -56,6 +57,9 @@ CONFIGS = {
              "rotation_ssg + translation_ssg forward, B=8/GPU (64 on 8 GPUs), N=2048, 10-ch"),
     "stress": ("pointnet2_cls_ssg", 128, 16384, "uniform3", "pointnet2_cls_ssg forward, B=128/GPU, N=16384"),
 }
+# MLP arithmetic per config: BASELINE config 5 (stress) asks for features/MLP in bf16, the
+# others are the reference's fp32
+DEFAULT_PRECISION = {"stress": "bf16"}
 
 
 def parse():
@@ -77,6 +81,8 @@ def parse():
                     help="graphed pipeline: keep the head on the compute stream")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="plain eager steps (default for single-head configs: pn2.pipeline)")
+    ap.add_argument("--precision", choices=("fp32", "bf16"), default=None,
+                    help="shared-MLP arithmetic (default: bf16 for --config stress, else fp32)")
     ap.add_argument("--geometry-cus", type=int, default=0,
                     help="CUs reserved for the FPS chain (0: streams share every CU)")
     return ap.parse_args()
@@ -157,12 +163,12 @@ def cpu_baseline(seconds):
                       "B=%d N=%d x %d forwards in %.1f s on %s" % (torch.__version__, Bs, N, n, el, cpu)}
 
 
-def load_traffic(cfg):
+def load_traffic(cfg, op="pn2_sa_mlp_max_f32"):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as fh:
             d = json.load(fh)
-        return d.get(cfg, {}).get("pn2_sa_mlp_max_f32")
+        return d.get(cfg, {}).get(op)
     except (OSError, ValueError):
         return None
 
@@ -181,6 +187,9 @@ def main():
     from pn2 import ops, shard
 
     head, B, N, kind, desc = CONFIGS[a.config]
+    prec = a.precision or DEFAULT_PRECISION.get(a.config, "fp32")
+    ctx = pn2.mlp_precision(prec)
+    ctx.__enter__()  # for the whole run (the pipeline captures its graphs under it)
     gB = B * world
     lo, hi = shard.shard_range(gB, rank, world)
     names, eager_models = build_models(a.config, dev)
@@ -256,14 +265,17 @@ def main():
         _, kt = timed(a.steps, True, eager_models)
 
     kern = kt.summary() if kt is not None else {}
-    mlp = kern.get("pn2_sa_mlp_max_f32")
+    mlp_name = "pn2_sa_mlp_max_bf16" if prec == "bf16" else "pn2_sa_mlp_max_f32"
+    mlp = kern.get(mlp_name)
     roof = None
     if mlp and mlp["ms"] > 0:
         achieved = mlp["flops"] / (mlp["ms"] * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(PEAK_SPLIT, 1),
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_SPLIT, 4),
-                "traffic": load_traffic(a.config),
-                "kernel": "pn2_sa_mlp_max_f32 (sa_chain_kernel / dense_split_kernel, split-bf16)",
+        peak = PEAK_BF16_MFMA if prec == "bf16" else PEAK_SPLIT
+        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1),
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "traffic": load_traffic(a.config, mlp_name),
+                "kernel": "%s (sa_chain_kernel / dense_split_kernel, %s)" % (
+                    mlp_name, "bf16, 1 MFMA per product" if prec == "bf16" else "split-bf16"),
                 "fp32_mfma_peak": PEAK_F32_MFMA,
                 "frac_of_fp32_mfma_peak": round(achieved / PEAK_F32_MFMA, 4),
                 "flops_per_launch": mlp["flops"] / mlp["launches"],
@@ -280,7 +292,9 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "point-clouds/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32 (MLP products as 6-term split bf16, fp32 accumulate; FPS/ball query f32)",
+            "dtype": ("bf16 (MLP operands bf16, fp32 accumulate / BN / max; FPS/ball query f32)"
+                      if prec == "bf16" else
+                      "f32 (MLP products as 6-term split bf16, fp32 accumulate; FPS/ball query f32)"),
             "data": "synthetic: seeded uniform clouds normalised to the unit sphere%s; seeded "
                     "random-init weights and BN statistics (eval mode)" % (
                         " + 7-way one-hot" if kind == "onehot10" else ""),

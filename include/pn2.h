@@ -40,7 +40,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 2
+#define PN2_ABI_VERSION 3
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -166,8 +166,23 @@ int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers, int n
                        int pool, float *out, int64_t ostride, float *workspace,
                        int64_t workspace_bytes, void *stream);
 
-/* Which kernel family served this thread's last successful pn2_sa_mlp_max_f32 call:
- * PN2_PATH_F32 (fp32 MFMA kernels) or PN2_PATH_SPLIT_BF16 (register-resident chain). */
+/* The same fused SA MLP in bf16 arithmetic (BASELINE config 5, "features/MLP in bf16"):
+ * every layer reads its input rounded to bf16 (round-to-nearest-even) and the hi plane of its
+ * pn2_pack_layer_split_bf16 image (= bf16(W)); products are exact, accumulation, BN, ReLU and
+ * the max are fp32, `out` is fp32.  Same arguments as pn2_sa_mlp_max_f32; every layer needs
+ * wt_split.  Chains the register-resident chain kernel or the dense-layer kernel do not cover
+ * return PN2_EUNSUPPORTED (no silent fp32 fallback).  Workspace: the _bf16 size query.
+ * Replaces nothing in the reference (it has no bf16 path): same interface as
+ * model/pointnet2_utils.py:167-172 at a lower precision, chosen by the caller. */
+int64_t pn2_sa_mlp_workspace_bytes_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers,
+                                        int nlayers);
+int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers, int nlayers,
+                        int pool, float *out, int64_t ostride, float *workspace,
+                        int64_t workspace_bytes, void *stream);
+
+/* Which kernel family served this thread's last successful pn2_sa_mlp_max_* call:
+ * PN2_PATH_F32 (fp32 MFMA kernels), PN2_PATH_SPLIT_BF16 (split-bf16 chain / dense kernels) or
+ * PN2_PATH_BF16 (pn2_sa_mlp_max_bf16). */
 /* ---- runtime: CU-partitioned streams (pipelined serving, pn2/pipeline.py) ---- */
 int pn2_device_cu_count(int device, int *count);
 /* A stream whose kernels run only on the CUs set in mask (bit i of word i/32 = CU i). */
@@ -176,6 +191,7 @@ int pn2_stream_destroy(void *stream);
 
 #define PN2_PATH_F32 1
 #define PN2_PATH_SPLIT_BF16 2
+#define PN2_PATH_BF16 3
 int pn2_sa_mlp_last_path(void);
 
 #ifdef __cplusplus

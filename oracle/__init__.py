@@ -144,3 +144,25 @@ def mlp_max(grouped, layers):
         y = (y - L["mean"]) * inv * L["gamma"] + L["beta"]
         x = np.maximum(y, 0.0)
     return x.max(axis=2)
+
+
+def bf16_round(x):
+    """float32 -> the nearest bfloat16 value (round-to-nearest-even), returned as float32."""
+    b = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    b = (b + 0x7FFF + ((b >> 16) & 1)) & 0xFFFF0000
+    return b.astype(np.uint32).view(np.float32)
+
+
+def mlp_max_bf16(grouped, layers):
+    """mlp_max in the bf16 arithmetic of pn2_sa_mlp_max_bf16 (BASELINE config 5; the reference
+    has no bf16 path, so this defines it): every layer's float32 input and its weights are
+    rounded to bfloat16 (RNE), the products summed exactly (float64 here, fp32 accumulation on
+    the GPU), bias / BatchNorm / ReLU applied to the fp32 sum.  Returns [B,S,Cout] float64."""
+    x = np.asarray(grouped, np.float32)
+    for L in layers:
+        W = bf16_round(L["W"]).astype(np.float64)
+        y = bf16_round(x).astype(np.float64) @ W.T + L["b"].astype(np.float64)
+        inv = 1.0 / np.sqrt(L["var"].astype(np.float64) + L["eps"])
+        y = (y - L["mean"]) * inv * L["gamma"] + L["beta"]
+        x = np.maximum(y, 0.0).astype(np.float32)
+    return x.max(axis=2).astype(np.float64)

@@ -61,18 +61,20 @@ struct ChainArgs {
     int lds_ring;  // byte offset of the workgroup weight ring (kStages stage buffers)
 };
 
+template <int NP>
 __device__ __forceinline__ Split load_w(const ChainLayer &L, int t, int kb, int lane) {
     const int64_t plane = (int64_t)L.tiles * L.kb * 64;
     const bf16x8 *p = L.w + ((int64_t)t * L.kb + kb) * 64 + lane;
     Split s;
     s.h = p[0];
-    s.m = p[plane];
-    s.l = p[2 * plane];
+    s.m = NP == 3 ? p[plane] : s.h;
+    s.l = NP == 3 ? p[2 * plane] : s.h;
     return s;
 }
 
 // BN + ReLU of a transposed hidden tile, split into the next layer's k-blocks 2t, 2t+1
 // al/be: this layer's BN scale/shift staged in LDS
+template <int NP>
 __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const float *al,
                                                 const float *be, int t, int h, Split &lo,
                                                 Split &hi) {
@@ -88,8 +90,8 @@ __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const floa
         y0[q] = chain_relu(__builtin_fmaf(acc[q], a4[q >> 2][q & 3], b4[q >> 2][q & 3]));
         y1[q] = chain_relu(__builtin_fmaf(acc[q + 8], a4[2 + (q >> 2)][q & 3], b4[2 + (q >> 2)][q & 3]));
     }
-    lo = split8(y0);
-    hi = split8(y1);
+    lo = splitN<NP>(y0);
+    hi = splitN<NP>(y1);
 }
 
 
@@ -107,24 +109,27 @@ __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const floa
 //      stage st is whole in LDS and no wave reads stage st-1 any more,
 //   4. copies its step of stage st+kStages-1 into stage st-1's buffer.
 // Past the last step the copies repeat the last step (same counts, never read).
-constexpr int kStepBytes = 3 * 1024;
 constexpr int kStages = 3;
-constexpr int kStageBytes = kChainWaves * kStepBytes;
+template <int NP> constexpr int step_bytes() { return NP * 1024; }  // one step: NP planes
+template <int NP> constexpr int stage_bytes() { return kChainWaves * step_bytes<NP>(); }
 
 // frag: the step's plane-0 fragment (wave-uniform); loff = lane * 16 -- the uniform-base +
 // lane-offset form lets the copy use a scalar base address (no per-copy vector address math)
+template <int NP>
 __device__ __forceinline__ void ring_issue(const bf16x8 *frag, int64_t plane, char *slot,
                                            unsigned loff) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < NP; ++p)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const char *>(frag + p * plane) + loff,
                                          (lds_void *)(slot + p * 1024), 16, 0, 0);
 }
 
-// step 2 above: this wave's copies of the kStages-2 younger stages may stay in flight
+// step 2 above: this wave's copies of the kStages-2 younger stages (NP each) may stay in flight
+template <int NP>
 __device__ __forceinline__ void stage_wait() {
     static_assert(kStages == 3, "stage_wait count");
-    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    if constexpr (NP == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
 }
 
 // Before a buffer is refilled, this wave's reads of it must have returned.  The compiler does
@@ -141,9 +146,10 @@ __device__ __forceinline__ void stage_barrier() {
 // KB0M > 0: the layer-0 input (<= KB0M k-blocks) is gathered once into registers and layer 0 runs
 // tile by tile from the ring like layers 1 and 2; KB0M == 0: layer 0 streams its input blocks
 // (k-outer, every output tile accumulating) with ordinary loads and the ring starts at layer 1.
-template <int T0, int T1, int KB0M>
+template <int T0, int T1, int KB0M, int NP>
 __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_eu(2))) void sa_chain_kernel(
     const ChainArgs A) {
+    constexpr int kStepBytes = step_bytes<NP>(), kStageBytes = stage_bytes<NP>();
     extern __shared__ __attribute__((aligned(16))) char csm[];
     constexpr int KB1 = 2 * T0, KB2 = 2 * T1;
     unsigned *cpool = reinterpret_cast<unsigned *>(csm);
@@ -172,7 +178,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     // Ring steps in consumption order: layers 0 (resident input only) and 1 block-major, layer 2
     // tile-major; source addresses come from scalar arithmetic on the layer's base.
     auto issue_l = [&](const ChainLayer &L, int t, int kb, char *dst) {
-        ring_issue(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64, dst, loff);
+        ring_issue<NP>(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64, dst, loff);
     };
     auto issue2 = [&](int z, char *dst) {  // layer-2 step z
         z = min(z, L2.tiles * KB2 - 1);
@@ -198,11 +204,11 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         if ((nread & (kChainWaves - 1)) == 0) {  // first step of a stage
             const int st = nread / kChainWaves;
             ring_fence();
-            stage_wait();
+            stage_wait<NP>();
             stage_barrier();
             issue_stage(st + kStages - 1);
         }
-        const Split w = ring_read(ring + ((nread / kChainWaves) % kStages) * kStageBytes +
+        const Split w = ring_readN<NP>(ring + ((nread / kChainWaves) % kStages) * kStageBytes +
                                       (nread & (kChainWaves - 1)) * kStepBytes, lane);
         ++nread;
         return w;
@@ -269,13 +275,13 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int kb = 0; kb < KB0M; ++kb) {
             if (kb < L0.kb) {
-                const Split xs = split8(x[kb]);
+                const Split xs = splitN<NP>(x[kb]);
 #pragma unroll
-                for (int t = 0; t < T0; ++t) acc[t] = mma6_wa(read_w(), xs, acc[t]);
+                for (int t = 0; t < T0; ++t) acc[t] = mma_wa<NP>(read_w(), xs, acc[t]);
             }
         }
 #pragma unroll
-        for (int t = 0; t < T0; ++t) hidden_epilogue(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+        for (int t = 0; t < T0; ++t) hidden_epilogue<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
     } else {
         // ---- layer 0 streamed: k-outer, every output tile accumulating (transposed)
         cfloatx16 acc[T0];
@@ -290,15 +296,15 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = xn[j];
             if (kb + 1 < L0.kb) load_x(kb + 1, xn);
-            const Split xs = split8(x);
+            const Split xs = splitN<NP>(x);
 #pragma unroll
-            for (int t = 0; t < T0; ++t) acc[t] = mma6_wa(load_w(L0, t, kb, lane), xs, acc[t]);
+            for (int t = 0; t < T0; ++t) acc[t] = mma_wa<NP>(load_w<NP>(L0, t, kb, lane), xs, acc[t]);
         }
         // layer 0's loads are all consumed: start the ring, then the epilogue hides its latency
 #pragma unroll
         for (int st = 0; st < kStages - 1; ++st) issue_stage(st);
 #pragma unroll
-        for (int t = 0; t < T0; ++t) hidden_epilogue(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+        for (int t = 0; t < T0; ++t) hidden_epilogue<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
     }
 
     // ---- layer 1: input in registers, k-outer (each input block dies after its use, so X1 and
@@ -313,9 +319,9 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int kb = 0; kb < KB1; ++kb)
 #pragma unroll
-            for (int t = 0; t < T1; ++t) acc[t] = mma6_wa(read_w(), X1[kb], acc[t]);
+            for (int t = 0; t < T1; ++t) acc[t] = mma_wa<NP>(read_w(), X1[kb], acc[t]);
 #pragma unroll
-        for (int t = 0; t < T1; ++t) hidden_epilogue(acc[t], al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
+        for (int t = 0; t < T1; ++t) hidden_epilogue<NP>(acc[t], al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
     }
 
     // ---- layer 2: standard orientation, pooled over the neighbourhood
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < KB2; ++kb) acc = mma6_wb(X2[kb], read_w(), acc);
+        for (int kb = 0; kb < KB2; ++kb) acc = mma_wb<NP>(X2[kb], read_w(), acc);
         // max over rows of relu(fma(acc, al, be)) = relu(fma(extreme, al, be)) exactly: fma with
         // a fixed al is monotone in acc (non-decreasing for al >= 0, else non-increasing) and
         // so is relu -- only the row max (al >= 0) or min of the accumulator is needed.
@@ -469,9 +475,9 @@ extern "C" int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t c
 // ------------------------------------------------------------------ host: dispatch
 namespace pn2 {
 
-template <int T0, int T1, int KB0M>
+template <int T0, int T1, int KB0M, int NP>
 static int launch_chain_sig(const ChainArgs &A, unsigned grid, size_t lds, hipStream_t st) {
-    hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
+    hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
     PN2_LAUNCH_CHECK("sa_chain_kernel");
     return PN2_OK;
 }
@@ -489,9 +495,9 @@ static int chain_kb0m(int T0, int T1, int kb0) {
 
 // 1: launched, 0: this chain is not eligible (caller uses the fp32 kernels), <0: error
 int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
-                     float *out, int64_t ostride, int64_t M, int64_t K, hipStream_t st) {
+                     float *out, int64_t ostride, int64_t M, int64_t K, int np, hipStream_t st) {
     if (const char *e = getenv("PN2_MLP_PATH"))
-        if (strcmp(e, "f32") == 0) return 0;
+        if (np == 3 && strcmp(e, "f32") == 0) return 0;
     if (nlayers != 3 || !pool) return 0;
     if (s.mode != PN2_SRC_GROUP_XYZ_FIRST && s.mode != PN2_SRC_GROUP_FEAT_FIRST) return 0;
     if (s.C > kMaxC) return 0;
@@ -548,10 +554,12 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     A.lds_bn = (int)((lds + 15) / 16 * 16);
     const size_t bn_bytes = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + coutL);
     A.lds_ring = (int)((A.lds_bn + bn_bytes + 15) / 16 * 16);
-    lds = (size_t)A.lds_ring + (size_t)kStages * kStageBytes;
+    lds = (size_t)A.lds_ring + (size_t)kStages * (np == 3 ? stage_bytes<3>() : stage_bytes<1>());
     int rc = PN2_EUNSUPPORTED;
-#define PN2_CHAIN_GO(a, b, c) \
-    if (T0 == a && T1 == b && KB0M == c) rc = launch_chain_sig<a, b, c>(A, grid, lds, st);
+#define PN2_CHAIN_GO(a, b, c)                                                             \
+    if (T0 == a && T1 == b && KB0M == c)                                                  \
+        rc = np == 3 ? launch_chain_sig<a, b, c, 3>(A, grid, lds, st)                     \
+                     : launch_chain_sig<a, b, c, 1>(A, grid, lds, st);
     PN2_CHAIN_SIGS(PN2_CHAIN_GO)
 #undef PN2_CHAIN_GO
     return rc == PN2_OK ? 1 : rc;

@@ -52,10 +52,10 @@ struct DenseSplitArgs {
     int64_t ostride;
 };
 
-template <int NTC>
+template <int NTC, int NP>
 __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitArgs A) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
-    constexpr int kFrag = 3 * NTC;                   // fragments per k-block
+    constexpr int kFrag = NP * NTC;                  // fragments per k-block
     constexpr int kStage = kKC * kFrag * 1024;       // bytes per weight stage
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
     };
 
     // ---- weight stages: stage c = k-blocks [c*kKC, c*kKC + kKC) of this workgroup's NTC tiles,
-    // fragment (kbl, i, p) at ((kbl * NTC + i) * 3 + p) KB
+    // fragment (kbl, i, p) at ((kbl * NTC + i) * NP + p) KB
     const int nst = (A.kb + kKC - 1) / kKC;
     const int64_t plane = (int64_t)A.tiles * A.kb * 64;
     const unsigned loff = (unsigned)lane * 16u;
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
         char *buf = stages + (c & 1) * kStage;
         for (int f = wave; f < kKC * kFrag; f += kDW) {
             const int kbl = f / kFrag, rem = f - kbl * kFrag;
-            const int i = rem / 3, p = rem - 3 * i;
+            const int i = rem / NP, p = rem - NP * i;
             const int kb = min(c * kKC + kbl, A.kb - 1);
             const bf16x8 *src = A.w + p * plane + ((int64_t)(ct0 + i) * A.kb + kb) * 64;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const char *>(src) + loff,
@@ -150,10 +150,10 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
 #pragma unroll
         for (int k = 0; k < kKC; ++k) {
             if (c * kKC + k < A.kb) {
-                const Split xs = split8(xa[k]);
+                const Split xs = splitN<NP>(xa[k]);
 #pragma unroll
                 for (int i = 0; i < NTC; ++i)
-                    acc[i] = mma6_wb(xs, ring_read(buf + (k * kFrag + 3 * i) * 1024, lane), acc[i]);
+                    acc[i] = mma_wb<NP>(xs, ring_readN<NP>(buf + (k * kFrag + NP * i) * 1024, lane), acc[i]);
             }
         }
 #pragma unroll
@@ -228,17 +228,17 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
     }
 }
 
-template <int NTC>
+template <int NTC, int NP>
 static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
-    const size_t lds = (size_t)2 * kKC * 3 * NTC * 1024 +
+    const size_t lds = (size_t)2 * kKC * NP * NTC * 1024 +
                        (A.pool_mode == 1 ? (size_t)(kDRows / A.K) * 32 * NTC * 4 : 0);
     dim3 grid((unsigned)((A.M + kDRows - 1) / kDRows), (unsigned)(A.tiles / NTC));
-    hipLaunchKernelGGL(dense_split_kernel<NTC>, grid, dim3(64 * kDW), lds, st, A);
+    hipLaunchKernelGGL((dense_split_kernel<NTC, NP>), grid, dim3(64 * kDW), lds, st, A);
     PN2_LAUNCH_CHECK("dense_split_kernel");
     return PN2_OK;
 }
 
-static int dense_split_layer(DenseSplitArgs &A, hipStream_t st) {
+static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
     // two output tiles per wave when that still leaves >= 2 workgroups per CU
     const int64_t rowblocks = (A.M + kDRows - 1) / kDRows;
     const int ntc = (A.tiles % 2 == 0 && rowblocks * (A.tiles / 2) >= 512) ? 2 : 1;
@@ -254,12 +254,13 @@ static int dense_split_layer(DenseSplitArgs &A, hipStream_t st) {
             if (e != hipSuccess) return set_error(PN2_EHIP, "dense_split: memset: %s", hipGetErrorString(e));
         }
     }
-    return ntc == 2 ? launch_dense_split<2>(A, st) : launch_dense_split<1>(A, st);
+    if (np == 1) return ntc == 2 ? launch_dense_split<2, 1>(A, st) : launch_dense_split<1, 1>(A, st);
+    return ntc == 2 ? launch_dense_split<2, 3>(A, st) : launch_dense_split<1, 3>(A, st);
 }
 
 // Widest hidden layer of a chain the split dense path runs layer by layer (0: not eligible).
-int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers) {
-    if (getenv("PN2_MLP_PATH") && strcmp(getenv("PN2_MLP_PATH"), "f32") == 0) return 0;
+int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np) {
+    if (np == 3 && getenv("PN2_MLP_PATH") && strcmp(getenv("PN2_MLP_PATH"), "f32") == 0) return 0;
     if (s.mode != PN2_SRC_GROUP_ALL && s.mode != PN2_SRC_ROWS) return 0;
     if (s.mode == PN2_SRC_GROUP_ALL && s.C > 16) return 0;
     int64_t w = 0;
@@ -274,8 +275,8 @@ int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int 
 // through the two [M][w] halves of the workspace.
 int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
                            float *out, int64_t ostride, float *ws, int64_t ws_bytes, int64_t M,
-                           int64_t K, hipStream_t st) {
-    const int64_t w = dense_split_width(s, layers, nlayers);
+                           int64_t K, int np, hipStream_t st) {
+    const int64_t w = dense_split_width(s, layers, nlayers, np);
     if (w == 0) return 0;
     if (nlayers > 1 && (!ws || ws_bytes < 2 * M * w * 4 || ((uintptr_t)ws & 15))) return 0;
     const bool vec_rows_ok = true;
@@ -313,7 +314,7 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
         A.K = (int)K;
         A.out = last ? out : ws + (l & 1) * M * w;
         A.ostride = last ? ostride : w;
-        const int rc = dense_split_layer(A, st);
+        const int rc = dense_split_layer(A, np, st);
         if (rc != PN2_OK) return rc;
     }
     return 1;

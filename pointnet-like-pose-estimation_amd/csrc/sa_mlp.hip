@@ -846,7 +846,7 @@ extern "C" int64_t pn2_sa_mlp_workspace_bytes(const pn2_sa_src *src, const pn2_m
                                               int nlayers) {
     int64_t M = 0, K = 1;
     if (validate(src, layers, nlayers, M, K) != PN2_OK) return -1;
-    const int64_t ds = nlayers > 1 ? dense_split_width(*src, layers, nlayers) : 0;
+    const int64_t ds = nlayers > 1 ? dense_split_width(*src, layers, nlayers, 3) : 0;
     return 2 * M * std::max(ds, workspace_width(*src, layers, nlayers, M, K)) * 4;
 }
 
@@ -877,13 +877,13 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
     if (M == 0) return PN2_OK;
     if (pool) PN2_REQUIRE(M % K == 0, "pn2_sa_mlp_max_f32: rows not a multiple of the group size");
     hipStream_t st = as_stream(stream);
-    rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, st);
+    rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, 3, st);
     if (rc != 0) {
         if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
         return rc < 0 ? rc : PN2_OK;
     }
     rc = try_launch_dense_split(*src, layers, nlayers, pool, out, ostride, workspace, workspace_bytes,
-                                M, K, st);
+                                M, K, 3, st);
     if (rc != 0) {
         if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
         return rc < 0 ? rc : PN2_OK;
@@ -915,5 +915,45 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
         }
         l0 = l1 + 1;
     }
+    return PN2_OK;
+}
+
+// bf16 arithmetic (BASELINE config 5, the large-N stress run): the same fused kernels with one
+// bf16 plane per operand -- activations rounded to bf16 (round-to-nearest-even) where a layer
+// reads them, weights = the hi plane of the split image, products exact, fp32 accumulation,
+// BN / ReLU / max in fp32, fp32 output.  No fp32 fallback: a chain neither the chain kernel nor
+// the dense-layer kernel covers is PN2_EUNSUPPORTED.
+extern "C" int64_t pn2_sa_mlp_workspace_bytes_bf16(const pn2_sa_src *src,
+                                                   const pn2_mlp_layer *layers, int nlayers) {
+    int64_t M = 0, K = 1;
+    if (validate(src, layers, nlayers, M, K) != PN2_OK) return -1;
+    const int64_t ds = nlayers > 1 ? dense_split_width(*src, layers, nlayers, 1) : 0;
+    return 2 * M * ds * 4;
+}
+
+extern "C" int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers,
+                                   int nlayers, int pool, float *out, int64_t ostride,
+                                   float *workspace, int64_t workspace_bytes, void *stream) {
+    int64_t M = 0, K = 1;
+    int rc = validate(src, layers, nlayers, M, K);
+    if (rc != PN2_OK) return rc;
+    PN2_REQUIRE(out, "pn2_sa_mlp_max_bf16: null out");
+    PN2_REQUIRE(ostride >= layers[nlayers - 1].cout, "pn2_sa_mlp_max_bf16: ostride");
+    for (int l = 0; l < nlayers; ++l)
+        PN2_REQUIRE(layers[l].wt_split && ((uintptr_t)layers[l].wt_split & 15) == 0,
+                    "pn2_sa_mlp_max_bf16: layer %d needs its 16-byte aligned split weight image", l);
+    if (M == 0) return PN2_OK;
+    if (pool) PN2_REQUIRE(M % K == 0, "pn2_sa_mlp_max_bf16: rows not a multiple of the group size");
+    hipStream_t st = as_stream(stream);
+    rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, 1, st);
+    if (rc == 0)
+        rc = try_launch_dense_split(*src, layers, nlayers, pool, out, ostride, workspace,
+                                    workspace_bytes, M, K, 1, st);
+    if (rc < 0) return rc;
+    if (rc == 0)
+        return set_error(PN2_EUNSUPPORTED,
+                         "pn2_sa_mlp_max_bf16: no bf16 kernel for this chain (%d layers, mode %d) "
+                         "or workspace too small", nlayers, src->mode);
+    g_last_path = PN2_PATH_BF16;
     return PN2_OK;
 }

@@ -68,6 +68,47 @@ __device__ __forceinline__ Split ring_read(const char *slot, int lane) {
     return w;
 }
 
+// ---- plane count NP: 3 = the fp32-accurate split above; 1 = plain bf16 arithmetic (operands
+// rounded to bf16 -- the hi plane -- products exact, fp32 accumulation), one MFMA per product.
+// NP == 1 leaves m / l as copies of h; nothing reads them, so they cost nothing.
+template <int NP>
+__device__ __forceinline__ Split splitN(const float (&x)[8]) {
+    if constexpr (NP == 3) {
+        return split8(x);
+    } else {
+        static_assert(NP == 1, "plane count");
+        Split s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s.h[j] = (__bf16)x[j];
+        s.m = s.h;
+        s.l = s.h;
+        return s;
+    }
+}
+template <int NP>
+__device__ __forceinline__ cfloatx16 mma_wa(const Split &w, const Split &x, cfloatx16 acc) {
+    if constexpr (NP == 3) return mma6_wa(w, x, acc);
+    else return PN2_MFMA16(w.h, x.h, acc, 0, 0, 0);
+}
+template <int NP>
+__device__ __forceinline__ cfloatx16 mma_wb(const Split &x, const Split &w, cfloatx16 acc) {
+    if constexpr (NP == 3) return mma6_wb(x, w, acc);
+    else return PN2_MFMA16(x.h, w.h, acc, 0, 0, 0);
+}
+// a step's NP plane fragments stored back to back (1 KB each) in LDS
+template <int NP>
+__device__ __forceinline__ Split ring_readN(const char *slot, int lane) {
+    if constexpr (NP == 3) {
+        return ring_read(slot, lane);
+    } else {
+        Split w;
+        w.h = reinterpret_cast<const bf16x8 *>(slot)[lane];
+        w.m = w.h;
+        w.l = w.h;
+        return w;
+    }
+}
+
 // lanes l and l^32 exchange x (the two halves of a 32x32 tile column)
 __device__ __forceinline__ float swap_halves(float x) {
     return __shfl_xor(x, 32);

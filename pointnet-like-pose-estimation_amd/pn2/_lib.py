@@ -48,6 +48,7 @@ SRC_GROUP_ALL = 2
 SRC_ROWS = 3
 PATH_F32 = 1
 PATH_SPLIT_BF16 = 2
+PATH_BF16 = 3
 
 # name -> (restype, argtypes); every symbol include/pn2.h declares
 SIGNATURES = {
@@ -73,9 +74,12 @@ SIGNATURES = {
     "pn2_sa_mlp_workspace_bytes": (_i64, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int]),
     "pn2_sa_mlp_max_f32": (_int, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int, _int, _vp,
                                   _i64, _vp, _i64, _vp]),
+    "pn2_sa_mlp_workspace_bytes_bf16": (_i64, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int]),
+    "pn2_sa_mlp_max_bf16": (_int, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int, _int, _vp,
+                                   _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lib = None
 
 

@@ -20,7 +20,7 @@ eager call + capture; training / autograd calls always run eagerly.
 """
 import torch
 
-from . import shard
+from . import ops, shard
 
 
 def _sig(args):
@@ -35,7 +35,7 @@ class GraphedForward:
 
     def _state_key(self, args):
         ts = list(self.model.parameters()) + list(self.model.buffers())
-        return (_sig(args),) + tuple((t.data_ptr(), t._version) for t in ts)
+        return (_sig(args), ops.current_precision()) + tuple((t.data_ptr(), t._version) for t in ts)
 
     def _eager(self, args):
         draws = []

@@ -18,6 +18,7 @@ Ops (reference code each replaces, in /root/reference/model/pointnet2_utils.py):
   pn2::sa_mlp_max_    gathered shared MLP + max :167-172, :211-218 (writes into `out`)
 """
 import contextlib
+import threading
 from typing import List, Optional, Tuple
 
 import torch
@@ -27,6 +28,30 @@ from . import _lib
 from ._lib import MlpLayer, SaSrc, check, load
 
 _L = load()  # fail at import, loudly, if the native library is unavailable
+
+# ------------------------------------------------------------------------------ MLP precision
+# "fp32": the reference's arithmetic (split-bf16 products at fp32 accuracy, or fp32 MFMA);
+# "bf16": bf16 operands, fp32 accumulation (BASELINE config 5) -- an explicit caller choice.
+PRECISIONS = ("fp32", "bf16")
+_prec = threading.local()
+
+
+def current_precision() -> str:
+    return getattr(_prec, "value", "fp32")
+
+
+@contextlib.contextmanager
+def mlp_precision(precision: str):
+    """Within this context (this thread) SA modules without their own ``mlp_precision``
+    attribute run their shared MLPs at `precision` ("fp32" or "bf16")."""
+    if precision not in PRECISIONS:
+        raise ValueError("pn2: precision must be one of %s, got %r" % (PRECISIONS, precision))
+    prev = current_precision()
+    _prec.value = precision
+    try:
+        yield
+    finally:
+        _prec.value = prev
 
 
 class KernelTimer:
@@ -338,11 +363,17 @@ def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K):
 def sa_mlp_max_direct(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor],
                 centers: Optional[Tensor], idx: Optional[Tensor], wts: List[Tensor],
                 alphas: List[Tensor], betas: List[Tensor], cins: List[int],
-                splits: List[Tensor]) -> None:
+                splits: List[Tensor], precision: str = "fp32") -> None:
     """Fused gather -> MLP (conv1x1+BN+ReLU)* -> max over each group, written channels-last
     into `out` ([G, >=cout] view with unit column stride; G = B*S groups, or B for
     group_all).  mode: 0 SSG grouping, 1 MSG grouping, 2 group_all.  splits: the
-    pack_layer_split images of the same layers (empty list: fp32 kernels only)."""
+    pack_layer_split images of the same layers (empty list: fp32 kernels only).
+    precision: "fp32" (pn2_sa_mlp_max_f32) or "bf16" (pn2_sa_mlp_max_bf16, needs splits)."""
+    if precision not in PRECISIONS:
+        raise ValueError("pn2::sa_mlp_max_: precision must be one of %s" % (PRECISIONS,))
+    bf16 = precision == "bf16"
+    if bf16 and not splits:
+        raise ValueError("pn2::sa_mlp_max_: bf16 needs the split weight images")
     _dev(points, "pn2::sa_mlp_max_")
     B, N, C = points.shape
     D = 0 if feature is None else feature.shape[2]
@@ -364,13 +395,15 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Tensor, feature: Optional[
         layers[i].wt_split = splits[i].data_ptr() if splits else 0
     if out.stride(-1) != 1:
         raise ValueError("pn2::sa_mlp_max_: out must have unit column stride")
-    ws_bytes = int(_L.pn2_sa_mlp_workspace_bytes(src, layers, n))
+    ws_fn = _L.pn2_sa_mlp_workspace_bytes_bf16 if bf16 else _L.pn2_sa_mlp_workspace_bytes
+    ws_bytes = int(ws_fn(src, layers, n))
     if ws_bytes < 0:
         check(-1, "pn2_sa_mlp_workspace_bytes")
     ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=points.device) if ws_bytes else None
     M = B * S * K
     flops = 2.0 * M * sum(cins[i] * wts[i].shape[1] for i in range(n))  # algorithmic, cin unpadded
-    _run("pn2_sa_mlp_max_f32", _L.pn2_sa_mlp_max_f32,
+    name = "pn2_sa_mlp_max_bf16" if bf16 else "pn2_sa_mlp_max_f32"
+    _run(name, getattr(_L, name),
          (src, layers, n, 1, out.data_ptr(), out.stride(-2), 0 if ws is None else ws.data_ptr(),
           ws_bytes, _stream(points)), points.device, flops=flops)
 
@@ -379,5 +412,5 @@ sa_mlp_max_ = torch.library.custom_op("pn2::sa_mlp_max_", sa_mlp_max_direct, mut
 
 
 @sa_mlp_max_.register_fake
-def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits):
+def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits, precision="fp32"):
     return None

@@ -273,7 +273,8 @@ class GraphedPipeline(PipelinedForward):
     def _state_key(self, x, extra):
         from .graphs import _sig
         ts = list(self.model.parameters()) + list(self.model.buffers())
-        return (_sig((x,) + tuple(extra)),) + tuple((t.data_ptr(), t._version) for t in ts)
+        return (_sig((x,) + tuple(extra)), ops.current_precision()) + tuple(
+            (t.data_ptr(), t._version) for t in ts)
 
     def _capture(self, x, extra, dev, draws):
         sl = _Slot()

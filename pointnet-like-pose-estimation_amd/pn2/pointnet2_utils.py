@@ -44,6 +44,13 @@ def _channels_last(feature):
     return f if f.stride(2) == 1 else f.contiguous()
 
 
+def _precision(module):
+    """The module's MLP arithmetic: its own ``mlp_precision`` if set, else the thread's
+    ``pn2.ops.mlp_precision`` context ("fp32" unless changed)."""
+    p = getattr(module, "mlp_precision", None)
+    return ops.current_precision() if p is None else p
+
+
 def _needs_autograd(module, *tensors):
     if module.training:
         return True
@@ -168,6 +175,7 @@ class PointNetSetAbstraction(nn.Module):
             self.mlp_bns.append(nn.BatchNorm2d(out_channel))
             last = out_channel
         self._pack_cache = {}
+        self.mlp_precision = None  # None: ops.mlp_precision context ("fp32" by default)
 
     def forward(self, points, feature):
         """points [B,C,N], feature [B,D,N] or None -> (new_points [B,C,S], new_feature
@@ -187,7 +195,7 @@ class PointNetSetAbstraction(nn.Module):
         if self.group_all:
             out = torch.empty(B, cout, device=dev, dtype=torch.float32)
             ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_ALL, pts, feat, None, None, wts, als, bes, cins,
-                            splits)
+                            splits, _precision(self))
             new_points = torch.zeros(B, C, 1, device=dev, dtype=torch.float32)
             return new_points, out.view(B, 1, cout).permute(0, 2, 1)
         S, K = self.point_number, self.sample_number
@@ -202,7 +210,7 @@ class PointNetSetAbstraction(nn.Module):
             span.finish([new_points], [new_points, idx])
         out = torch.empty(B * S, cout, device=dev, dtype=torch.float32)
         ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
-                        cins, splits)
+                        cins, splits, _precision(self))
         return new_points.permute(0, 2, 1), out.view(B, S, cout).permute(0, 2, 1)
 
     def _forward_autograd(self, points, feature):
@@ -241,6 +249,7 @@ class PointNetSetAbstractionMsg(nn.Module):
             self.conv_blocks.append(convs)
             self.bn_blocks.append(bns)
         self._pack_cache = [{} for _ in mlp_list]
+        self.mlp_precision = None  # None: ops.mlp_precision context ("fp32" by default)
 
     def forward(self, points, feature):
         if _needs_autograd(self, points, feature):
@@ -267,12 +276,13 @@ class PointNetSetAbstractionMsg(nn.Module):
                         for r, k in zip(self.radius_list, self.sample_number_list)]
             span.finish([new_points], [new_points] + idxs)
         out = torch.empty(B * S, total, device=dev, dtype=torch.float32)
+        prec = _precision(self)
         col = 0
         for i, idx in enumerate(idxs):
             wts, als, bes, cins, splits = chains[i]
             cout = wts[-1].shape[1]
             ops.sa_mlp_max_direct(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
-                            new_points, idx, wts, als, bes, cins, splits)
+                            new_points, idx, wts, als, bes, cins, splits, prec)
             col += cout
         return new_points.permute(0, 2, 1), out.view(B, S, total).permute(0, 2, 1)
 
