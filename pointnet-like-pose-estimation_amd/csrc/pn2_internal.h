@@ -31,12 +31,16 @@ constexpr int kMaxC = 16;  // point dims (xyz + one-hot) held in registers
 // np: bf16 planes per operand -- 3 = fp32-accurate split products, 1 = plain bf16 products
 // sa_chain.hip: 1 launched, 0 not eligible, <0 error
 int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
-                     float *out, int64_t ostride, int64_t M, int64_t K, int np, hipStream_t st);
+                     float *out, int64_t ostride, int64_t M, int64_t K, int np, float *ws,
+                     int64_t ws_bytes, hipStream_t st);
 // sa_dense.hip: split-bf16 layer-by-layer path for group_all / dense-row chains
 int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np);
 int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
                            float *out, int64_t ostride, float *ws, int64_t ws_bytes, int64_t M,
                            int64_t K, int np, hipStream_t st);
+int launch_layer0_prepass(const pn2_sa_src &s, const pn2_mlp_layer &L0, float *z, hipStream_t st);
+// bytes of workspace the chain kernel's layer-0 pre-pass needs for this chain (0: not used)
+int64_t chain_prepass_bytes(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np);
 
 // --------------------------------------------------------------- device: reference sum orders
 // torch.sum(x**2, -1) over the channel axis, reproduced bit-for-bit (torch 2.10 CPU, AVX512);

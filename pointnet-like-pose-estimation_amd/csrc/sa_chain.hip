@@ -59,6 +59,13 @@ struct ChainArgs {
     int64_t ostride;
     int lds_bn;    // byte offset of the staged BN scale/shift
     int lds_ring;  // byte offset of the workgroup weight ring (kStages stage buffers)
+    // KB0M < 0 (layer 0 pre-transformed): z [B*N][32*T0] = W0 . [xyz | features] of every source
+    // point (launch_layer0_prepass); the xyz columns of W0 in the fp32 image `wt` (input channel
+    // k of xyz at row w0x_row + k); u [groups][32*T0] = W0_xyz . centroid staged at lds_u
+    const float *z;
+    const float *w0x;
+    int w0x_row;
+    int lds_u, u_groups;
 };
 
 template <int NP>
@@ -172,6 +179,25 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
     if (A.pool_mode == 1)
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
+    const unsigned g0 = (unsigned)(blockIdx.x * kChainRows) / (unsigned)A.K;  // first group
+    float *ulds = reinterpret_cast<float *>(csm + A.lds_u);
+    if constexpr (KB0M < 0) {
+        // u[g][c] = sum_k W0[c][xyz k] * centroid[g][k]: the centroid's share of layer 0, which
+        // the per-point pre-pass (z) could not subtract
+        const unsigned Gn = (unsigned)A.M / (unsigned)A.K;
+        for (int e = tid; e < A.u_groups * 32 * T0; e += 64 * kChainWaves) {
+            const int gl = e / (32 * T0), c = e - gl * (32 * T0);
+            const unsigned g = g0 + gl;
+            float u = 0.f;
+            if (g < Gn)
+                for (int k = 0; k < A.C; ++k) {
+                    const int row = A.w0x_row + k;
+                    u = __builtin_fmaf(A.w0x[((int64_t)(row >> 1) * (32 * T0) + c) * 2 + (row & 1)],
+                                       A.src.ctr[(int64_t)g * A.C + k], u);
+                }
+            ulds[e] = u;
+        }
+    }
     __syncthreads();
     char *ring = csm + A.lds_ring;
     const unsigned loff = (unsigned)lane * 16u;
@@ -252,7 +278,48 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     };
 
     Split X1[2 * T0];
-    if constexpr (KB0M > 0) {
+    if constexpr (KB0M < 0) {
+        // ---- layer 0 pre-transformed: acc = z[point] - u[group], already in the transposed
+        // accumulator layout (register 4m + i of lane (r, h) = channel 32t + 8m + 4h + i)
+#pragma unroll
+        for (int st = 0; st < kStages - 1; ++st) issue_stage(st);
+        const float *zrow = A.z + ((int64_t)b * s.N + n) * (32 * T0);
+        const float *urow = ulds + (int)(g - g0) * (32 * T0);
+        // Tile t+1's z / u loads are issued while tile t is split (one tile of lookahead).  The
+        // loads are read-only, so the compiler would hoist every tile's loads to the top and
+        // spill at 2 waves/SIMD: the address of tile t+1 is tied (opaque asm) to tile t-1's
+        // result, which bounds the loads in flight to two tiles.
+        cfloatx4 zc[4], uc[4];
+        auto load_tile = [&](int o, cfloatx4 (&zq)[4], cfloatx4 (&uq)[4]) {
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                zq[m] = *reinterpret_cast<const cfloatx4 *>(zrow + o + 8 * m);
+                uq[m] = *reinterpret_cast<const cfloatx4 *>(urow + o + 8 * m);
+            }
+        };
+        load_tile(4 * h, zc, uc);
+        unsigned dep = 0;
+#pragma unroll
+        for (int t = 0; t < T0; ++t) {
+            cfloatx4 zn[4], un[4];
+            if (t + 1 < T0) {
+                int o = 32 * (t + 1) + 4 * h;
+                asm volatile("" : "+v"(o) : "v"(dep));
+                load_tile(o, zn, un);
+            }
+            cfloatx16 acc;
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[4 * m + i] = zc[m][i] - uc[m][i];
+            int zero = 0;  // the BN scale / shift reads of tile t wait for tile t-1 likewise
+            asm volatile("" : "+v"(zero) : "v"(dep));
+            hidden_epilogue<NP>(acc, al0 + zero, be0 + zero, t, h, X1[2 * t], X1[2 * t + 1]);
+            dep = __builtin_bit_cast(unsigned, __builtin_shufflevector(X1[2 * t].h, X1[2 * t].h, 0, 1));
+#pragma unroll
+            for (int m = 0; m < 4; ++m) zc[m] = zn[m], uc[m] = un[m];
+        }
+    } else if constexpr (KB0M > 0) {
         // ---- layer 0 from registers: the whole input gathered once (raw fp32), then k-outer
         // (each block split once, every output tile accumulating) with weights from the ring
         float x[KB0M][8];
@@ -399,8 +466,10 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 // SSG [64,64,128] [128,128,256], MSG [32,32,64] [64,64,128] [64,96,128] [128,128,256]
 // (T0, T1, KB0M): KB0M = 1 for xyz-only inputs (sa1 layers), 9 for 131/138-channel inputs
 // (SSG/pose sa2), 0 = streamed layer-0 input (any width)
+// -1 = layer 0 pre-transformed per source point (wide first layers, see chain_use_prepass)
 #define PN2_CHAIN_SIGS(X) \
-    X(1, 1, 1) X(2, 2, 1) X(2, 3, 1) X(4, 4, 9) X(1, 1, 0) X(2, 2, 0) X(2, 3, 0) X(4, 4, 0)
+    X(1, 1, 1) X(2, 2, 1) X(2, 3, 1) X(4, 4, 9) X(1, 1, 0) X(2, 2, 0) X(2, 3, 0) X(4, 4, 0) \
+    X(2, 2, -1) X(4, 4, -1)
 
 }  // namespace pn2
 
@@ -487,31 +556,74 @@ static int launch_chain_sig(const ChainArgs &A, unsigned grid, size_t lds, hipSt
 static int chain_kb0m(int T0, int T1, int kb0) {
     int best = -1;
 #define PN2_CHAIN_HAS(a, b, c) \
-    if (T0 == a && T1 == b && (c == 0 ? best < 0 : (kb0 <= c && (best <= 0 || c < best)))) best = c;
+    if (c >= 0 && T0 == a && T1 == b && (c == 0 ? best < 0 : (kb0 <= c && (best <= 0 || c < best)))) best = c;
     PN2_CHAIN_SIGS(PN2_CHAIN_HAS)
 #undef PN2_CHAIN_HAS
     return best;
 }
 
-// 1: launched, 0: this chain is not eligible (caller uses the fp32 kernels), <0: error
-int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
-                     float *out, int64_t ostride, int64_t M, int64_t K, int np, hipStream_t st) {
-    if (const char *e = getenv("PN2_MLP_PATH"))
-        if (np == 3 && strcmp(e, "f32") == 0) return 0;
-    if (nlayers != 3 || !pool) return 0;
-    if (s.mode != PN2_SRC_GROUP_XYZ_FIRST && s.mode != PN2_SRC_GROUP_FEAT_FIRST) return 0;
-    if (s.C > kMaxC) return 0;
+// Layer-0 pre-pass (KB0M = -1).  Layer 0 is linear in [xyz - centroid | features], so
+// W0 . row = W0 . [xyz | features](point) - W0_xyz . centroid: the first term depends only on
+// the source point and is computed once per point (launch_layer0_prepass) instead of once per
+// (group, neighbour) row -- K*S/N times fewer products (16x at SSG sa2) -- and the chain gathers
+// it in place of the raw row.  Used for wide first layers (>= 5 k-blocks) of fp32 chains with
+// a compiled (T0, T1, -1) instance when the rows outnumber the points 4:1, given workspace.
+static bool chain_use_prepass(const pn2_sa_src &s, const pn2_mlp_layer *layers, int T0, int T1,
+                              int kb0, int64_t M, int np) {
+    if (np != 3 || kb0 < 5 || s.C < 1 || s.C > kMaxC || !layers[0].wt) return false;
+    if (const char *e = getenv("PN2_CHAIN_PREPASS"))
+        if (strcmp(e, "0") == 0) return false;
+    if (4 * s.B * s.N > M) return false;
+    bool has = false;
+#define PN2_CHAIN_HAS(a, b, c) \
+    if (c < 0 && T0 == a && T1 == b) has = true;
+    PN2_CHAIN_SIGS(PN2_CHAIN_HAS)
+#undef PN2_CHAIN_HAS
+    return has;
+}
+
+static bool chain_shape(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
+                        int &T0, int &T1, int (&kbs)[3]) {
+    if (nlayers != 3 || !pool) return false;
+    if (s.mode != PN2_SRC_GROUP_XYZ_FIRST && s.mode != PN2_SRC_GROUP_FEAT_FIRST) return false;
+    if (s.C > kMaxC) return false;
     for (int l = 0; l < 3; ++l)
-        if (!layers[l].wt_split || ((uintptr_t)layers[l].wt_split & 15)) return 0;
-    const int T0 = (int)(layers[0].cout / 32), T1 = (int)(layers[1].cout / 32);
-    // k-blocks per layer (the first layer's rows are [xyz | features], see split_in_channel)
-    int kbs[3];
+        if (!layers[l].wt_split || ((uintptr_t)layers[l].wt_split & 15)) return false;
+    T0 = (int)(layers[0].cout / 32);
+    T1 = (int)(layers[1].cout / 32);
     kbs[0] = (int)pn2_layer_split_kblocks(layers[0].cin, s.C);
     kbs[1] = (int)((layers[1].cin + 15) / 16);
     kbs[2] = (int)((layers[2].cin + 15) / 16);
-    if (kbs[0] < 1) return 0;
-    const int KB0M = chain_kb0m(T0, T1, kbs[0]);
+    return kbs[0] >= 1;
+}
+
+int64_t chain_prepass_bytes(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np) {
+    int T0, T1, kbs[3];
+    if (!chain_shape(s, layers, nlayers, 1, T0, T1, kbs)) return 0;
+    const int64_t M = s.B * s.S * s.K;
+    if (!chain_use_prepass(s, layers, T0, T1, kbs[0], M, np)) return 0;
+    return s.B * s.N * layers[0].cout * 4;
+}
+
+// 1: launched, 0: this chain is not eligible (caller uses the fp32 kernels), <0: error
+int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
+                     float *out, int64_t ostride, int64_t M, int64_t K, int np, float *ws,
+                     int64_t ws_bytes, hipStream_t st) {
+    if (const char *e = getenv("PN2_MLP_PATH"))
+        if (np == 3 && strcmp(e, "f32") == 0) return 0;
+    // k-blocks per layer (the first layer's rows are [xyz | features], see split_in_channel)
+    int T0, T1, kbs[3];
+    if (!chain_shape(s, layers, nlayers, pool, T0, T1, kbs)) return 0;
+    int KB0M = chain_kb0m(T0, T1, kbs[0]);
     if (KB0M < 0) return 0;
+    const int64_t zbytes = s.B * s.N * layers[0].cout * 4;
+    const bool pre = chain_use_prepass(s, layers, T0, T1, kbs[0], M, np) && ws &&
+                     ws_bytes >= zbytes && ((uintptr_t)ws & 15) == 0;
+    if (pre) {
+        const int rc = launch_layer0_prepass(s, layers[0], ws, st);
+        if (rc != PN2_OK) return rc;
+        KB0M = -1;
+    }
     ChainArgs A;
     memset(&A, 0, sizeof(A));
     A.src = s;
@@ -531,6 +643,11 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     A.ostride = ostride;
     A.vec_feat = (s.D > 0 && s.D % 4 == 0 && ((uintptr_t)s.feat & 15) == 0 && s.fn % 4 == 0 &&
                   s.fb % 4 == 0) ? 1 : 0;
+    if (pre) {
+        A.z = ws;
+        A.w0x = layers[0].wt;
+        A.w0x_row = (int)(layers[0].cin - s.C);  // the fp32 image's rows are [features | xyz]
+    }
     const int64_t coutL = layers[2].cout;
     size_t lds = 0;
     if (K == 8 || K == 16 || K == 32) {
@@ -555,6 +672,11 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     const size_t bn_bytes = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + coutL);
     A.lds_ring = (int)((A.lds_bn + bn_bytes + 15) / 16 * 16);
     lds = (size_t)A.lds_ring + (size_t)kStages * (np == 3 ? stage_bytes<3>() : stage_bytes<1>());
+    if (pre) {  // u for every group a workgroup's rows touch
+        A.u_groups = (int)((kChainRows + K - 1) / K + 1);
+        A.lds_u = (int)((lds + 15) / 16 * 16);
+        lds = (size_t)A.lds_u + (size_t)A.u_groups * layers[0].cout * 4;
+    }
     int rc = PN2_EUNSUPPORTED;
 #define PN2_CHAIN_GO(a, b, c)                                                             \
     if (T0 == a && T1 == b && KB0M == c)                                                  \

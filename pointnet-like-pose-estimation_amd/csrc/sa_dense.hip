@@ -50,6 +50,7 @@ struct DenseSplitArgs {
     int pool_mode;  // 0: registers (K = 8, 16), 1: LDS (K | kDRows), 2: HBM atomics
     float *out;
     int64_t ostride;
+    int raw;        // 1: out = A . W^T as accumulated (no BN / ReLU; the chain's layer-0 pre-pass)
 };
 
 template <int NTC, int NP>
@@ -168,12 +169,13 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
 #pragma unroll
     for (int i = 0; i < NTC; ++i) {
         const int col = 32 * (ct0 + i) + r;
-        const float al = A.alpha[col], be = A.beta[col];
+        const float al = A.raw ? 1.f : A.alpha[col], be = A.raw ? 0.f : A.beta[col];
         if (!A.pool) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int row = slab_row + (q & 3) + 8 * (q >> 2) + 4 * h;
-                if (row < A.M) A.out[(int64_t)row * A.ostride + col] = chain_relu(__builtin_fmaf(acc[i][q], al, be));
+                if (row < A.M)
+                    A.out[(int64_t)row * A.ostride + col] = A.raw ? acc[i][q] : chain_relu(__builtin_fmaf(acc[i][q], al, be));
             }
             continue;
         }
@@ -256,6 +258,28 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
     }
     if (np == 1) return ntc == 2 ? launch_dense_split<2, 1>(A, st) : launch_dense_split<1, 1>(A, st);
     return ntc == 2 ? launch_dense_split<2, 3>(A, st) : launch_dense_split<1, 3>(A, st);
+}
+
+// The chain kernel's layer-0 pre-pass (sa_chain.hip, KB0M < 0): z[b*N + n][c] = sum_k W0[c][k] *
+// x_k(b, n) over the raw [xyz | features] row of every source point (no bias / BN / ReLU), with
+// the fp32-accurate split products.  z is [B*N][cout0] fp32 at `z` (16-byte aligned).
+int launch_layer0_prepass(const pn2_sa_src &s, const pn2_mlp_layer &L0, float *z, hipStream_t st) {
+    DenseSplitArgs A;
+    memset(&A, 0, sizeof(A));
+    A.mode = 1;
+    A.pts = s.pts; A.pb = s.pb; A.pn = s.pn; A.pc = s.pc;
+    A.feat = s.feat; A.fb = s.fb; A.fn = s.fn;
+    A.N = (int)s.N; A.C = (int)s.C; A.D = (int)s.D;
+    A.vec = (s.D == 0 || (s.D % 4 == 0 && ((uintptr_t)s.feat & 15) == 0 && s.fn % 4 == 0 &&
+                          s.fb % 4 == 0)) ? 1 : 0;
+    A.kb = (int)pn2_layer_split_kblocks(L0.cin, s.C);
+    A.w = reinterpret_cast<const bf16x8 *>(L0.wt_split);
+    A.tiles = (int)(L0.cout / 32);
+    A.M = (int)(s.B * s.N);
+    A.out = z;
+    A.ostride = L0.cout;
+    A.raw = 1;
+    return dense_split_layer(A, 3, st);
 }
 
 // Widest hidden layer of a chain the split dense path runs layer by layer (0: not eligible).

@@ -847,7 +847,8 @@ extern "C" int64_t pn2_sa_mlp_workspace_bytes(const pn2_sa_src *src, const pn2_m
     int64_t M = 0, K = 1;
     if (validate(src, layers, nlayers, M, K) != PN2_OK) return -1;
     const int64_t ds = nlayers > 1 ? dense_split_width(*src, layers, nlayers, 3) : 0;
-    return 2 * M * std::max(ds, workspace_width(*src, layers, nlayers, M, K)) * 4;
+    return std::max(2 * M * std::max(ds, workspace_width(*src, layers, nlayers, M, K)) * 4,
+                    chain_prepass_bytes(*src, layers, nlayers, 3));
 }
 
 static int run_plan(const pn2_sa_src &cur, const pn2_mlp_layer *layers, int l0, int l1, int pool,
@@ -877,7 +878,8 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
     if (M == 0) return PN2_OK;
     if (pool) PN2_REQUIRE(M % K == 0, "pn2_sa_mlp_max_f32: rows not a multiple of the group size");
     hipStream_t st = as_stream(stream);
-    rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, 3, st);
+    rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, 3, workspace,
+                          workspace_bytes, st);
     if (rc != 0) {
         if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
         return rc < 0 ? rc : PN2_OK;
@@ -945,7 +947,8 @@ extern "C" int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *l
     if (M == 0) return PN2_OK;
     if (pool) PN2_REQUIRE(M % K == 0, "pn2_sa_mlp_max_bf16: rows not a multiple of the group size");
     hipStream_t st = as_stream(stream);
-    rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, 1, st);
+    rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, 1, workspace,
+                          workspace_bytes, st);
     if (rc == 0)
         rc = try_launch_dense_split(*src, layers, nlayers, pool, out, ostride, workspace,
                                     workspace_bytes, M, K, 1, st);

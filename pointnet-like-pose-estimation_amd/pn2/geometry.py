@@ -105,14 +105,16 @@ class Span:
 
 
 # ----------------------------------------------------------------------------- provided FPS
-# pn2.pipeline runs a batch's FPS chain ahead of its forward; the SA modules then take the
-# precomputed (centroids, packed centroids, packed points) instead of drawing and sampling.
+# pn2.pipeline runs a batch's geometry chain (FPS + ball queries of every SA layer) ahead of its
+# forward; the SA modules then take the precomputed (centroids, packed centroids, packed
+# points, neighbour indices per radius) instead of drawing, sampling and querying.
 _tls = threading.local()
 
 
 @contextlib.contextmanager
 def provide(entries):
-    """entries: {id(module): (input data_ptr, new_points, ctr_packed, pts_packed)}."""
+    """entries: {id(module): (input data_ptr, new_points, ctr_packed, pts_packed, idxs)};
+    idxs: the ball-query indices per radius of the module, or None (the module queries)."""
     prev = getattr(_tls, "entries", None)
     _tls.entries = entries
     try:
@@ -128,8 +130,8 @@ def take(module, pts):
     entries = getattr(_tls, "entries", None)
     if not entries or id(module) not in entries:
         return None
-    ptr, newp, cpk, ppk = entries.pop(id(module))
+    ptr, newp, cpk, ppk, idxs = entries.pop(id(module))
     if ptr != pts.data_ptr():
         raise RuntimeError("pn2.pipeline: the SA module was called on a different point tensor "
                            "than the one its FPS was precomputed for")
-    return newp, cpk, ppk
+    return newp, cpk, ppk, idxs

@@ -150,15 +150,22 @@ class PipelinedForward:
         return hook
 
     def _fps_chain(self, x):
-        """FPS of every SA layer for input x ([B, C, N]); draws in layer order."""
+        """Geometry of every SA layer for input x ([B, C, N]): FPS (draws in layer order) and
+        the ball query of each radius -- both read only coordinates, so a batch's whole
+        geometry runs ahead of its MLPs."""
         entries = {}
         pts = x.permute(0, 2, 1)
         for sa in self.sas:
             if getattr(sa, "group_all", False):
                 break
-            B, N, _ = pts.shape
+            B, N, C = pts.shape
             _, newp, cpk, ppk = ops.fps_direct(pts, sa.point_number, shard.device_start(B, N, x.device))
-            entries[id(sa)] = (pts.data_ptr(), newp, cpk, ppk)
+            if isinstance(sa, PointNetSetAbstractionMsg):
+                rk = list(zip(sa.radius_list, sa.sample_number_list))
+            else:
+                rk = [(sa.radius, sa.sample_number)]
+            idxs = [ops.ball_query_direct(ppk, cpk, C, r, k) for r, k in rk]
+            entries[id(sa)] = (pts.data_ptr(), newp, cpk, ppk, idxs)
             pts = newp
         return entries
 
@@ -205,8 +212,8 @@ class PipelinedForward:
                         nxt = self._fps_chain(batches[i + 1])
                         nxt_ev = geo.record_event()
                 main.wait_event(ev)
-                for _, newp, cpk, ppk in entries.values():
-                    for t in (newp, cpk, ppk):
+                for _, newp, cpk, ppk, idxs in entries.values():
+                    for t in [newp, cpk, ppk] + idxs:
                         t.record_stream(main)
                 with torch.cuda.stream(main), geometry.provide(entries):
                     extra = () if extras is None else tuple(extras[i])

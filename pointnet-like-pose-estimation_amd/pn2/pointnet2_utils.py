@@ -199,10 +199,10 @@ class PointNetSetAbstraction(nn.Module):
             new_points = torch.zeros(B, C, 1, device=dev, dtype=torch.float32)
             return new_points, out.view(B, 1, cout).permute(0, 2, 1)
         S, K = self.point_number, self.sample_number
-        pre = geometry.take(self, pts)  # FPS precomputed by pn2.pipeline
+        pre = geometry.take(self, pts)  # FPS (+ ball query) precomputed by pn2.pipeline
         if pre is not None:
-            new_points, cpk, ppk = pre
-            idx = ops.ball_query_direct(ppk, cpk, C, self.radius, K)
+            new_points, cpk, ppk, idxs = pre
+            idx = idxs[0] if idxs else ops.ball_query_direct(ppk, cpk, C, self.radius, K)
         else:
             with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
                 _, new_points, cpk, ppk = ops.fps_direct(pts, S, _draw_start(B, N, dev))
@@ -264,11 +264,12 @@ class PointNetSetAbstractionMsg(nn.Module):
                               False)
                   for i in range(len(self.radius_list))]
         total = sum(ch[0][-1].shape[1] for ch in chains)
-        pre = geometry.take(self, pts)  # FPS precomputed by pn2.pipeline
+        pre = geometry.take(self, pts)  # FPS (+ ball queries) precomputed by pn2.pipeline
         if pre is not None:
-            new_points, cpk, ppk = pre
-            idxs = [ops.ball_query_direct(ppk, cpk, C, r, k)
-                    for r, k in zip(self.radius_list, self.sample_number_list)]
+            new_points, cpk, ppk, idxs = pre
+            if not idxs:
+                idxs = [ops.ball_query_direct(ppk, cpk, C, r, k)
+                        for r, k in zip(self.radius_list, self.sample_number_list)]
         else:
             with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
                 _, new_points, cpk, ppk = ops.fps_direct(pts, S, _draw_start(B, N, dev))

@@ -24,6 +24,7 @@ CASES = [
     (3, 8, 8, 40, 256, [64, 96, 128], True, True),        # K=8
     (10, 0, 128, 16, 512, [64, 64, 128], False, True),    # pose layout, K=128
     (3, 4, 96, 8, 256, [64, 64, 128], False, True),       # K=96: HBM atomics
+    (3, 96, 32, 32, 256, [64, 64, 128], True, True),      # MSG, wide layer 0 -> pre-pass (T0=2)
     (3, 16, 32, 16, 256, [96, 64, 64], False, False),     # no chain signature -> fp32
     (3, 0, 32, 8, 128, [64, 128], False, False),          # 2 layers -> fp32
 ]
@@ -46,9 +47,11 @@ def _oracle_layers(convs, bns):
     return out
 
 
-@pytest.mark.parametrize("path", ["chain", "f32"])
+@pytest.mark.parametrize("path", ["chain", "chain_noprepass", "f32"])
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_sa_mlp_vs_oracle(case, path, monkeypatch):
+    """chain: default dispatch (wide first layers take the per-point layer-0 pre-pass, cases 1,
+    6); chain_noprepass: PN2_CHAIN_PREPASS=0 (layer 0 on the gathered rows); f32: fp32 MFMA."""
     import pn2
     from pn2 import _lib
     C, D, K, S, N, mlp, msg, chain_ok = CASES[case]
@@ -56,6 +59,10 @@ def test_sa_mlp_vs_oracle(case, path, monkeypatch):
         monkeypatch.setenv("PN2_MLP_PATH", "f32")
     else:
         monkeypatch.delenv("PN2_MLP_PATH", raising=False)
+    if path == "chain_noprepass":
+        monkeypatch.setenv("PN2_CHAIN_PREPASS", "0")
+    else:
+        monkeypatch.delenv("PN2_CHAIN_PREPASS", raising=False)
     B, radius = 2, 0.35
     pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 100 + case)
     gen = torch.Generator().manual_seed(200 + case)
@@ -75,7 +82,7 @@ def test_sa_mlp_vs_oracle(case, path, monkeypatch):
     with torch.no_grad():
         newp, newf = sa(x.to(DEV), None if f is None else f.to(DEV))
     torch.cuda.synchronize()
-    want_path = _lib.PATH_SPLIT_BF16 if (chain_ok and path == "chain") else _lib.PATH_F32
+    want_path = _lib.PATH_SPLIT_BF16 if (chain_ok and path != "f32") else _lib.PATH_F32
     assert _lib.load().pn2_sa_mlp_last_path() == want_path
 
     ps = x.permute(0, 2, 1)  # the module's own (point-contiguous) view
