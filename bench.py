@@ -79,6 +79,8 @@ def parse():
                     help="eager pipeline: run the head on its own stream (default off there)")
     ap.add_argument("--no-tail", action="store_true",
                     help="graphed pipeline: keep the head on the compute stream")
+    ap.add_argument("--slots", type=int, default=3,
+                    help="graphed pipeline: batches in flight (geometry runs slots-1 ahead)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="plain eager steps (default for single-head configs: pn2.pipeline)")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default=None,
@@ -206,7 +208,7 @@ def main():
         from pn2.pipeline import GraphedPipeline, PipelinedForward
         if not a.eager_pipeline:
             pf = GraphedPipeline(eager_models[0], geometry_cus=a.geometry_cus,
-                                 tail=not a.no_tail)
+                                 tail=not a.no_tail, nslots=a.slots)
         else:
             pf = PipelinedForward(eager_models[0], geometry_cus=a.geometry_cus,
                                   tail="auto" if a.tail else False)

@@ -240,7 +240,7 @@ _MODE = "thread_local"
 
 
 class _Slot:
-    """Static buffers and graphs of one pipeline slot (batches i with i % 2 == slot)."""
+    """Static buffers and graphs of one pipeline slot (batches i with i % nslots == slot)."""
 
 
 class GraphedPipeline(PipelinedForward):
@@ -248,20 +248,24 @@ class GraphedPipeline(PipelinedForward):
 
     The eager pipeline issues ~25 launches plus the SA modules' Python per batch; on MI355X that
     host time (~0.5 ms per SSG B=32 batch) is as long as the GPU work, so the GPU idles.  Here
-    each of two slots (batch i uses slot i % 2) holds static inputs and three captured graphs:
-      fps   the batch's FPS chain (``_fps_chain``), replayed on the geometry stream;
+    each of ``nslots`` slots (batch i uses slot i % nslots) holds static inputs and three
+    captured graphs:
+      fps   the batch's geometry (``_fps_chain``: FPS + ball queries), replayed on the geometry
+            stream ``nslots - 1`` batches ahead of the compute stream;
       sa    the forward up to the last SA layer, replayed on the compute stream;
       head  the rest of the forward, replayed on a third stream with the geometry CUs (``tail``;
             with tail=False, head is part of sa).
     The capture is split at the last SA layer by a forward hook (capture_end / capture_begin).
-    Events order the slot reuse: batch i+2's fps waits for batch i's sa (it overwrites the
-    slot's inputs and FPS outputs), batch i+2's sa waits for batch i's head (they share a memory
-    pool).  Static memory makes the tail safe for every head here, including the translation
+    Events order the slot reuse: batch i+nslots's fps waits for batch i's sa (it overwrites the
+    slot's inputs and geometry outputs), batch i+nslots's sa waits for batch i's head (they share
+    a memory pool).  With 3 slots (default) the geometry chain has two batches of slack: at SSG
+    its ~340 us (under MLP contention) is as long as the compute stream's work, so with 2 slots
+    any jitter on either stream stalls the other.  Static memory makes the tail safe for every head here, including the translation
     heads' ``mean`` (see PipelinedForward).
 
     RNG and results: as PipelinedForward.  The first batch of a new input signature (or after
     any parameter change) runs through the eager pipeline -- its real result, its draws -- and
-    both slots are captured after it; the captures draw nothing.  Every replayed batch takes its
+    every slot is captured after it; the captures draw nothing.  Every replayed batch takes its
     draws on the host in batch order (shard.draw_start, so shard.batch_shard applies) and uploads
     them into the slot before its fps replay.  Outputs are cloned out of the static buffers on
     the stream that produced them, so they stay valid.
@@ -272,8 +276,11 @@ class GraphedPipeline(PipelinedForward):
     stream (59.5k).
     """
 
-    def __init__(self, model, geometry_cus=0, tail=True):
+    def __init__(self, model, geometry_cus=0, tail=True, nslots=3):
         super().__init__(model, geometry_cus, bool(tail))
+        if nslots < 2:
+            raise ValueError("pn2.pipeline: GraphedPipeline needs at least 2 slots")
+        self.nslots = int(nslots)
         self._key = None
         self._slots = None
 
@@ -354,7 +361,8 @@ class GraphedPipeline(PipelinedForward):
             with shard.start_source(record):
                 outs = self._run_eager(batches[:1], None if extras is None else extras[:1],
                                        post, False)
-            self._slots = [self._capture(batches[0], extra_of(0), dev, draws) for _ in range(2)]
+            self._slots = [self._capture(batches[0], extra_of(0), dev, draws)
+                           for _ in range(self.nslots)]
             self._key = self._state_key(batches[0], extra_of(0))
             first = 1
         if first == len(batches):
@@ -363,14 +371,15 @@ class GraphedPipeline(PipelinedForward):
         caller = torch.cuda.current_stream(dev)
         for st in (geo, main, tail):
             st.wait_stream(caller)
-        ev_fps, ev_sa, ev_head = [None, None], [None, None], [None, None]
+        ns = self.nslots
+        ev_fps, ev_sa, ev_head = [None] * ns, [None] * ns, [None] * ns
         starts = self._draw_all(len(batches) - first)
 
         def issue_fps(j):
-            s = j % 2
+            s = j % ns
             sl = self._slots[s]
             with torch.cuda.stream(geo):
-                if ev_sa[s] is not None:  # batch j-2 is done with the slot's inputs
+                if ev_sa[s] is not None:  # batch j-ns is done with the slot's inputs
                     geo.wait_event(ev_sa[s])
                 sl.x.copy_(batches[j], non_blocking=True)
                 sl.start_buf.copy_(starts[j - first], non_blocking=True)
@@ -378,15 +387,17 @@ class GraphedPipeline(PipelinedForward):
                 ev_fps[s] = geo.record_event()
 
         with torch.no_grad():
-            issue_fps(first)
+            # the geometry runs ns-1 batches ahead of the compute stream
+            for j in range(first, min(first + ns - 1, len(batches))):
+                issue_fps(j)
             for i in range(first, len(batches)):
-                s = i % 2
+                s = i % ns
                 sl = self._slots[s]
-                if i + 1 < len(batches):
-                    issue_fps(i + 1)
+                if i + ns - 1 < len(batches):
+                    issue_fps(i + ns - 1)
                 with torch.cuda.stream(main):
                     main.wait_event(ev_fps[s])
-                    if ev_head[s] is not None:  # batch i-2's head is done with the pool
+                    if ev_head[s] is not None:  # batch i-ns's head is done with the pool
                         main.wait_event(ev_head[s])
                     for d, e in zip(sl.extra, extra_of(i)):
                         d.copy_(e, non_blocking=True)
