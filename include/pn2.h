@@ -40,7 +40,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 3
+#define PN2_ABI_VERSION 4
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -120,7 +120,13 @@ typedef struct pn2_mlp_layer {
     int64_t cin;
     int64_t cout;
     const void *wt_split; /* pn2_pack_layer_split_bf16 image of the same W, or NULL */
+    int64_t flags;        /* PN2_LAYER_* bits, 0 = the SA layers' conv + BN + ReLU       */
 } pn2_mlp_layer;
+
+/* Layer without the ReLU: out = alpha * (W x) + beta (PointNetEncoder's conv3 + bn3 before its
+ * max, /root/reference/model/pointnet_utils.py:125-127).  Served by the split dense-layer
+ * kernels only (group_all / rows sources); other kernels reject it with PN2_EUNSUPPORTED. */
+#define PN2_LAYER_NO_RELU 1
 
 /* The same W packed for the split-bf16 chain kernel: three bf16 planes (hi, mid, lo with
  * W = hi + mid + lo to 2^-24 relative), each [cout/32][kblocks][64 lanes][8] in MFMA fragment

@@ -588,7 +588,9 @@ static bool chain_shape(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nl
     if (s.mode != PN2_SRC_GROUP_XYZ_FIRST && s.mode != PN2_SRC_GROUP_FEAT_FIRST) return false;
     if (s.C > kMaxC) return false;
     for (int l = 0; l < 3; ++l)
-        if (!layers[l].wt_split || ((uintptr_t)layers[l].wt_split & 15)) return false;
+        if (!layers[l].wt_split || ((uintptr_t)layers[l].wt_split & 15) ||
+            (layers[l].flags & PN2_LAYER_NO_RELU))
+            return false;
     T0 = (int)(layers[0].cout / 32);
     T1 = (int)(layers[1].cout / 32);
     kbs[0] = (int)pn2_layer_split_kblocks(layers[0].cin, s.C);

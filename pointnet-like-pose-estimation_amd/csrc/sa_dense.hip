@@ -51,7 +51,26 @@ struct DenseSplitArgs {
     float *out;
     int64_t ostride;
     int raw;        // 1: out = A . W^T as accumulated (no BN / ReLU; the chain's layer-0 pre-pass)
+    int norelu;     // 1: out = alpha * (A . W^T) + beta, no ReLU (signed values: pooled as keys)
 };
+
+// Signed max through unsigned atomics: key() is monotone from float order to uint order (and
+// key(anything) > 0, so a zeroed pool is below every value); unkey() inverts it.
+__device__ __forceinline__ unsigned fkey(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float funkey(unsigned k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+__global__ void unkey_kernel(float *out, int64_t ostride, int64_t G, int cols) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= G * cols) return;
+    const int64_t g = e / cols;
+    float *p = out + g * ostride + (e - g * cols);
+    *p = funkey(__float_as_uint(*p));
+}
 
 template <int NTC, int NP>
 __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitArgs A) {
@@ -174,14 +193,19 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int row = slab_row + (q & 3) + 8 * (q >> 2) + 4 * h;
-                if (row < A.M)
-                    A.out[(int64_t)row * A.ostride + col] = A.raw ? acc[i][q] : chain_relu(__builtin_fmaf(acc[i][q], al, be));
+                if (row < A.M) {
+                    const float y = __builtin_fmaf(acc[i][q], al, be);
+                    A.out[(int64_t)row * A.ostride + col] = A.raw ? acc[i][q] : (A.norelu ? y : chain_relu(y));
+                }
             }
             continue;
         }
         // max over rows of relu(fma(acc, al, be)) = relu(fma(row max (al >= 0) or min, al, be))
         const bool up = al >= 0.f;
-        auto fin = [&](float mx, float mn) { return chain_relu(__builtin_fmaf(up ? mx : mn, al, be)); };
+        auto fin = [&](float mx, float mn) {
+            const float y = __builtin_fmaf(up ? mx : mn, al, be);
+            return A.norelu ? y : chain_relu(y);
+        };
         if (A.pool_mode == 0) {  // K = 8 or 16: rows 8k..8k+7 are registers 4k..4k+3
             float mx[4], mn[4];
 #pragma unroll
@@ -204,6 +228,21 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
             }
             continue;
         }
+        if (A.pool_mode == 2 && (slab_row + 31 >= A.M || (unsigned)slab_row / (unsigned)A.K !=
+                                                             (unsigned)(slab_row + 31) / (unsigned)A.K)) {
+            // K % 32 != 0: this slab straddles a group boundary or the end of the rows (whose
+            // zero-filled rows must not pool) -- one atomic per valid row
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = slab_row + (q & 3) + 8 * (q >> 2) + 4 * h;
+                if (row < A.M) {
+                    const float m = fin(acc[i][q], acc[i][q]);
+                    atomicMax(reinterpret_cast<unsigned *>(A.out + (int64_t)((unsigned)row / (unsigned)A.K) * A.ostride + col),
+                              A.norelu ? fkey(m) : __float_as_uint(m));
+                }
+            }
+            continue;
+        }
         float mx = acc[i][0], mn = acc[i][0];
 #pragma unroll
         for (int q = 1; q < 16; ++q) {
@@ -211,13 +250,14 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
             mn = fminf(mn, acc[i][q]);
         }
         const float m = fin(fmaxf(mx, swap_halves(mx)), fminf(mn, swap_halves(mn)));
+        // ReLU output >= +0: its bits order as uints; signed (norelu) values go through fkey
+        const unsigned mk = A.norelu ? fkey(m) : __float_as_uint(m);
         if (h == 0 && slab_row < A.M) {
             const unsigned gg = (unsigned)slab_row / (unsigned)A.K;
             if (A.pool_mode == 1)
-                atomicMax(reinterpret_cast<unsigned *>(opool) + ((int)gg - row0 / A.K) * ncols + 32 * i + r,
-                          __float_as_uint(m));
+                atomicMax(reinterpret_cast<unsigned *>(opool) + ((int)gg - row0 / A.K) * ncols + 32 * i + r, mk);
             else
-                atomicMax(reinterpret_cast<unsigned *>(A.out + (int64_t)gg * A.ostride + col), __float_as_uint(m));
+                atomicMax(reinterpret_cast<unsigned *>(A.out + (int64_t)gg * A.ostride + col), mk);
         }
     }
     if (A.pool && A.pool_mode == 1) {
@@ -225,7 +265,9 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
         for (int e = tid; e < gpb * ncols; e += 64 * kDW) {
             const int gl = e / ncols, c = e - gl * ncols;
             const unsigned gg = (unsigned)(row0 / A.K + gl);
-            if (gg < G) A.out[(int64_t)gg * A.ostride + 32 * ct0 + c] = opool[e];
+            if (gg < G)
+                A.out[(int64_t)gg * A.ostride + 32 * ct0 + c] =
+                    A.norelu ? funkey(__float_as_uint(opool[e])) : opool[e];
         }
     }
 }
@@ -256,8 +298,16 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
             if (e != hipSuccess) return set_error(PN2_EHIP, "dense_split: memset: %s", hipGetErrorString(e));
         }
     }
-    if (np == 1) return ntc == 2 ? launch_dense_split<2, 1>(A, st) : launch_dense_split<1, 1>(A, st);
-    return ntc == 2 ? launch_dense_split<2, 3>(A, st) : launch_dense_split<1, 3>(A, st);
+    int rc;
+    if (np == 1) rc = ntc == 2 ? launch_dense_split<2, 1>(A, st) : launch_dense_split<1, 1>(A, st);
+    else rc = ntc == 2 ? launch_dense_split<2, 3>(A, st) : launch_dense_split<1, 3>(A, st);
+    if (rc == PN2_OK && A.pool && A.pool_mode == 2 && A.norelu) {  // keys -> floats
+        const int64_t G = A.M / A.K, cols = 32 * (int64_t)A.tiles;
+        hipLaunchKernelGGL(unkey_kernel, dim3((unsigned)((G * cols + 255) / 256)), dim3(256), 0, st,
+                           A.out, A.ostride, G, (int)cols);
+        PN2_LAUNCH_CHECK("unkey_kernel");
+    }
+    return rc;
 }
 
 // The chain kernel's layer-0 pre-pass (sa_chain.hip, KB0M < 0): z[b*N + n][c] = sum_k W0[c][k] *
@@ -335,6 +385,7 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
         A.tiles = (int)(layers[l].cout / 32);
         A.M = (int)M;
         A.pool = last ? pool : 0;
+        A.norelu = (layers[l].flags & PN2_LAYER_NO_RELU) ? 1 : 0;
         A.K = (int)K;
         A.out = last ? out : ws + (l & 1) * M * w;
         A.ostride = last ? ostride : w;

@@ -890,6 +890,10 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
         if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
         return rc < 0 ? rc : PN2_OK;
     }
+    for (int l = 0; l < nlayers; ++l)
+        if (layers[l].flags & PN2_LAYER_NO_RELU)
+            return set_error(PN2_EUNSUPPORTED, "pn2_sa_mlp_max_f32: layer %d without ReLU needs the split "
+                             "dense-layer path (group_all / rows source, split weight images)", l);
     g_last_path = PN2_PATH_F32;
     const int64_t w = workspace_width(*src, layers, nlayers, M, K);
     if (w > 0)

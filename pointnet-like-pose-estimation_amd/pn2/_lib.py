@@ -27,7 +27,7 @@ class Pn2Error(RuntimeError):
 
 class MlpLayer(ctypes.Structure):
     _fields_ = [("wt", _vp), ("alpha", _vp), ("beta", _vp), ("cin", _i64), ("cout", _i64),
-                ("wt_split", _vp)]
+                ("wt_split", _vp), ("flags", _i64)]
 
 
 class SaSrc(ctypes.Structure):
@@ -49,6 +49,7 @@ SRC_ROWS = 3
 PATH_F32 = 1
 PATH_SPLIT_BF16 = 2
 PATH_BF16 = 3
+LAYER_NO_RELU = 1
 
 # name -> (restype, argtypes); every symbol include/pn2.h declares
 SIGNATURES = {
@@ -79,7 +80,7 @@ SIGNATURES = {
                                    _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _lib = None
 
 

@@ -360,30 +360,46 @@ def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K):
     return s
 
 
-def sa_mlp_max_direct(out: Tensor, mode: int, points: Tensor, feature: Optional[Tensor],
+def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature: Optional[Tensor],
                 centers: Optional[Tensor], idx: Optional[Tensor], wts: List[Tensor],
                 alphas: List[Tensor], betas: List[Tensor], cins: List[int],
-                splits: List[Tensor], precision: str = "fp32") -> None:
+                splits: List[Tensor], precision: str = "fp32", flags: Optional[List[int]] = None,
+                rows: Optional[Tensor] = None, pool: bool = True) -> None:
     """Fused gather -> MLP (conv1x1+BN+ReLU)* -> max over each group, written channels-last
     into `out` ([G, >=cout] view with unit column stride; G = B*S groups, or B for
-    group_all).  mode: 0 SSG grouping, 1 MSG grouping, 2 group_all.  splits: the
+    group_all).  mode: 0 SSG grouping, 1 MSG grouping, 2 group_all, 3 rows (`rows` [B, R, cin]
+    with unit column stride: B groups of R rows, `points` unused).  splits: the
     pack_layer_split images of the same layers (empty list: fp32 kernels only).
-    precision: "fp32" (pn2_sa_mlp_max_f32) or "bf16" (pn2_sa_mlp_max_bf16, needs splits)."""
+    precision: "fp32" (pn2_sa_mlp_max_f32) or "bf16" (pn2_sa_mlp_max_bf16, needs splits).
+    flags: per-layer PN2_LAYER_* bits (LAYER_NO_RELU).  pool=False: `out` gets every row's
+    last-layer output ([M, >=cout], group_all / rows sources)."""
     if precision not in PRECISIONS:
         raise ValueError("pn2::sa_mlp_max_: precision must be one of %s" % (PRECISIONS,))
     bf16 = precision == "bf16"
     if bf16 and not splits:
         raise ValueError("pn2::sa_mlp_max_: bf16 needs the split weight images")
-    _dev(points, "pn2::sa_mlp_max_")
-    B, N, C = points.shape
-    D = 0 if feature is None else feature.shape[2]
-    if mode == _lib.SRC_GROUP_ALL:
-        S, K = 1, N
+    if mode == _lib.SRC_ROWS:
+        _dev(rows, "pn2::sa_mlp_max_")
+        if rows.dim() != 3 or rows.stride(2) != 1 or rows.stride(0) != rows.shape[1] * rows.stride(1):
+            raise ValueError("pn2::sa_mlp_max_: rows must be [B, R, cin] with unit column stride "
+                             "and uniform row stride")
+        B, K = rows.shape[0], rows.shape[1]
+        src = _src(mode, None, None, None, None, rows.view(B * K, -1) if B * K else rows[0],
+                   B, K, 0, 0, 1, K)
+        dev_t = rows
+        S = 1
     else:
-        S, K = idx.shape[1], idx.shape[2]
-        idx = idx.contiguous()
-        centers = centers.contiguous()
-    src = _src(mode, points, feature, centers, idx, None, B, N, C, D, S, K)
+        _dev(points, "pn2::sa_mlp_max_")
+        B, N, C = points.shape
+        D = 0 if feature is None else feature.shape[2]
+        if mode == _lib.SRC_GROUP_ALL:
+            S, K = 1, N
+        else:
+            S, K = idx.shape[1], idx.shape[2]
+            idx = idx.contiguous()
+            centers = centers.contiguous()
+        src = _src(mode, points, feature, centers, idx, None, B, N, C, D, S, K)
+        dev_t = points
     n = len(wts)
     layers = (MlpLayer * n)()
     for i in range(n):
@@ -393,24 +409,26 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Tensor, feature: Optional[
         layers[i].cin = cins[i]
         layers[i].cout = wts[i].shape[1]  # [cin_pad/2, cout, 2]
         layers[i].wt_split = splits[i].data_ptr() if splits else 0
+        layers[i].flags = int(flags[i]) if flags else 0
     if out.stride(-1) != 1:
         raise ValueError("pn2::sa_mlp_max_: out must have unit column stride")
     ws_fn = _L.pn2_sa_mlp_workspace_bytes_bf16 if bf16 else _L.pn2_sa_mlp_workspace_bytes
     ws_bytes = int(ws_fn(src, layers, n))
     if ws_bytes < 0:
         check(-1, "pn2_sa_mlp_workspace_bytes")
-    ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=points.device) if ws_bytes else None
+    ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev_t.device) if ws_bytes else None
     M = B * S * K
     flops = 2.0 * M * sum(cins[i] * wts[i].shape[1] for i in range(n))  # algorithmic, cin unpadded
     name = "pn2_sa_mlp_max_bf16" if bf16 else "pn2_sa_mlp_max_f32"
     _run(name, getattr(_L, name),
-         (src, layers, n, 1, out.data_ptr(), out.stride(-2), 0 if ws is None else ws.data_ptr(),
-          ws_bytes, _stream(points)), points.device, flops=flops)
+         (src, layers, n, 1 if pool else 0, out.data_ptr(), out.stride(-2),
+          0 if ws is None else ws.data_ptr(), ws_bytes, _stream(dev_t)), dev_t.device, flops=flops)
 
 
 sa_mlp_max_ = torch.library.custom_op("pn2::sa_mlp_max_", sa_mlp_max_direct, mutates_args=("out",))
 
 
 @sa_mlp_max_.register_fake
-def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits, precision="fp32"):
+def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits, precision="fp32",
+      flags=None, rows=None, pool=True):
     return None

@@ -101,3 +101,19 @@ HEAD_CASES = {
     'translation_ssg': ('translation_ssg', 2, 1024, 'onehot10', 103, 203),
     'rotation_msg': ('rotation_msg', 2, 1024, 'onehot10', 104, 204),
 }
+
+# PointNet-v1 cases (/root/reference/model/pointnet_utils.py and the v1
+# heads): name -> (head module, B, N, cloud kind, weight seed, get_model kwargs)
+V1_CASES = {
+    'pointnet_cls': ('pointnet_cls', 4, 1024, 'uniform3', 300, {}),
+    'rotation_v1': ('rotation', 2, 1024, 'onehot10', 301, {}),
+    'translation_v1': ('translation', 2, 1024, 'onehot10', 302, {}),
+    'sign_v1': ('sign', 2, 1024, 'onehot10', 303, {}),
+    'width_v1': ('width', 2, 1024, 'onehot10', 304, {'normal_channel': False}),
+    # pose.py with both T-Nets on a 3-channel cloud (D > 3 with transform=True fails in the
+    # reference: its cat is along the points axis, pose.py:57) and the classify tail
+    'pose_v1': ('pose', 2, 1024, 'uniform3', 305,
+                {'mlp_list': [64, 64, 64, 128, 1024], 'linear_list': [512, 256, 2],
+                 'classify': True, 'num_category': 0, 'normal_channel': False,
+                 'transform': True, 'feat_trans': True}),
+}

@@ -12,6 +12,8 @@ Files:
   head_<case>.npz   per-SA-layer outputs and head outputs for cases.HEAD_CASES (eval mode,
                     seeded weights + BN statistics; the weights are regenerated from the seed
                     and pinned by a state_dict SHA-256)
+  v1_<case>.npz     PointNet-v1 heads (cases.V1_CASES): encoder / T-Net / head outputs
+(`make_goldens.py v1` regenerates only the v1 files, etc.)
   meta.json         torch version, CPU capability, MKL/oneDNN versions, thread count
 """
 import json
@@ -95,11 +97,61 @@ def gen_heads(importlib):
         print("head", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
 
 
+def gen_v1(importlib):
+    """PointNet-v1 heads (pointnet_utils.py + pointnet_cls / rotation / translation / sign):
+    the encoder's (global feature, input transform, feature transform), the T-Nets' outputs and
+    the head outputs, eval mode.  sign.py misses `import torch` (sign.py:1-3, like sign_ssg), so
+    the harness sets it on the module without editing the file."""
+    for name, (head, B, N, kind, wseed, kw) in cases.V1_CASES.items():
+        mod = importlib.import_module(head)
+        if not hasattr(mod, "torch"):
+            mod.torch = torch
+        model = cases.build_head(mod.get_model, wseed, **kw)
+        x = cases.cloud(kind, B, N, wseed + 7)
+        xin = x.permute(0, 2, 1).contiguous()
+        rec = {"input": xin.numpy(), "state_hash": np.array(cases.state_hash(model))}
+        acts = {}
+
+        def hook(tag):
+            def f(_m, _inp, out):
+                outs = out if isinstance(out, tuple) else (out,)
+                for i, o in enumerate(outs):
+                    acts["%s_%d" % (tag, i)] = o.detach().contiguous().numpy()
+            return f
+        for tag, sub in (("feat", "feat"), ("tnet", "feat.tnet"), ("ftnet", "feat.ftnet"),
+                         ("ftnet", "ftnet"), ("tnet", "tnet")):
+            m = model
+            try:
+                for part in sub.split("."):
+                    m = getattr(m, part)
+            except AttributeError:
+                continue
+            m.register_forward_hook(hook(tag))
+        args = [xin]
+        if head == "translation":
+            mean = torch.randn(B, 3, generator=torch.Generator().manual_seed(wseed + 9))
+            rec["mean"] = mean.numpy()
+            args.append(mean)
+        with torch.no_grad():
+            out = model(*args)
+        outs = out if isinstance(out, tuple) else (out,)
+        for i, o in enumerate(outs):
+            rec["out%d" % i] = o.detach().numpy()
+        rec.update(acts)
+        np.savez_compressed(os.path.join(HERE, "v1_%s.npz" % name), **rec)
+        print("v1", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
+
+
 def main():
     torch.set_num_threads(8)
     P, importlib = _ref()
-    gen_index(P)
-    gen_heads(importlib)
+    only = sys.argv[1:]
+    if not only or "index" in only:
+        gen_index(P)
+    if not only or "heads" in only:
+        gen_heads(importlib)
+    if not only or "v1" in only:
+        gen_v1(importlib)
     meta = {
         "torch": torch.__version__,
         "cpu_capability": torch.backends.cpu.get_cpu_capability(),

@@ -1,0 +1,199 @@
+"""PointNet-v1 path: pn2/pointnet_utils.py (drop-in for
+/root/reference/model/pointnet_utils.py) and the v1 head restatements (pn2/heads_v1.py),
+against goldens produced by the reference itself (tests/golden/make_goldens.py v1).
+
+CPU tests: seeded weights reproduce the reference's state_dict, the autograd (torch) path
+reproduces the goldens, eval on a CPU tensor raises (no CPU fallback), and the reference's own
+v1 head files run unchanged on the drop-in.  GPU tests: eval-mode heads on the split-bf16
+dense-layer kernels against the goldens, and the kernel features the v1 path adds (rows
+source, unpooled output, PN2_LAYER_NO_RELU signed max) against torch fp32 on the same device.
+
+Tolerance (float, as tests/test_gpu_sa.py): |got - ref| <= rtol * |ref| + rtol * max|ref|,
+rtol = 1e-5 for encoder features / T-Net outputs, 1e-4 for head outputs (two more GEMM layers
+of fp32 library rounding differences)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import cases
+from conftest import golden_names, load_golden
+
+REF = "/root/reference/model"
+
+
+def _build(name):
+    from pn2.heads_v1 import HEADS_V1
+    head, B, N, kind, wseed, kw = cases.V1_CASES[name]
+    return cases.build_head(HEADS_V1[head], wseed, **kw), head
+
+
+def _args(g, dev):
+    args = [torch.from_numpy(g["input"]).to(dev)]
+    if "mean" in g:
+        args.append(torch.from_numpy(g["mean"]).to(dev))
+    return args
+
+
+def _hooks(model, acts):
+    for tag, sub in (("feat", "feat"), ("tnet", "feat.tnet"), ("ftnet", "feat.ftnet"),
+                     ("ftnet", "ftnet"), ("tnet", "tnet")):
+        m = model
+        try:
+            for part in sub.split("."):
+                m = getattr(m, part)
+        except AttributeError:
+            continue
+
+        def f(_m, _i, out, tag=tag):
+            for i, o in enumerate(out if isinstance(out, tuple) else (out,)):
+                acts["%s_%d" % (tag, i)] = o.detach().cpu().numpy()
+        m.register_forward_hook(f)
+
+
+def assert_close(got, want, rtol):
+    got = np.asarray(got, np.float64)
+    want = np.asarray(want, np.float64)
+    np.testing.assert_allclose(got, want, rtol=rtol, atol=rtol * max(float(np.abs(want).max()), 1e-30))
+
+
+def _check(g, out, acts, rtol_feat, rtol_out):
+    for k, v in acts.items():
+        assert k in g, k
+        assert_close(v, g[k], rtol_feat)
+    outs = out if isinstance(out, tuple) else (out,)
+    for i, o in enumerate(outs):
+        o = o.detach().cpu().numpy()
+        if o.dtype == np.int64:
+            np.testing.assert_array_equal(o, g["out%d" % i])
+        else:
+            assert_close(o, g["out%d" % i], rtol_out)
+
+
+# ---------------------------------------------------------------------------------- CPU
+@pytest.mark.parametrize("name", golden_names("v1_"))
+def test_v1_heads_rebuild_reference_weights(name):
+    model, _ = _build(name)
+    assert cases.state_hash(model) == str(load_golden("v1_%s.npz" % name)["state_hash"])
+
+
+@pytest.mark.parametrize("name", golden_names("v1_"))
+def test_v1_autograd_path_matches_goldens(name):
+    """Grad-enabled eval forward = the reference's torch formulation, on the CPU."""
+    g = load_golden("v1_%s.npz" % name)
+    model, _ = _build(name)
+    acts = {}
+    _hooks(model, acts)
+    out = model(*_args(g, "cpu"))
+    _check(g, out, acts, 1e-6, 1e-6)
+
+
+def test_v1_eval_on_cpu_raises():
+    from pn2.heads_v1 import HEADS_V1
+    from pn2.pointnet_utils import PointNetEncoder
+    for model, x in ((PointNetEncoder(channel=3).eval(), torch.rand(2, 3, 64)),
+                     (HEADS_V1["sign"]().eval(), torch.rand(2, 10, 64))):
+        with pytest.raises(RuntimeError, match="ROCm device tensors only"):
+            with torch.no_grad():
+                model(x)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present")
+@pytest.mark.parametrize("head", ["pointnet_cls", "rotation", "pose"])
+def test_reference_v1_heads_import_drop_in_unchanged(head, monkeypatch):
+    """The reference's own v1 head files, with `pointnet_utils` resolving to the drop-in, load
+    a reference-built state_dict strictly and run (autograd path) to the reference's numbers;
+    eval without autograd reaches the kernels (CPU tensor -> loud error).  (translation / sign
+    / width keep their whole conv stack in the head file: only pn2.heads_v1 accelerates them.)"""
+    import importlib
+    import pn2.pointnet_utils as ours
+    monkeypatch.setattr(sys, "dont_write_bytecode", True)
+    monkeypatch.syspath_prepend(REF)
+    kw = {"mlp_list": [64, 64, 128, 1024], "linear_list": [512, 256, 2], "transform": True,
+          "feat_trans": True, "num_category": 0, "normal_channel": False} if head == "pose" else {}
+    for m in ("pointnet_utils", head):
+        sys.modules.pop(m, None)
+    torch.manual_seed(5)
+    ref = importlib.import_module(head).get_model(**kw).eval()
+    sys.modules.pop(head, None)
+    monkeypatch.setitem(sys.modules, "pointnet_utils", ours)
+    mod = importlib.import_module(head)
+    model = mod.get_model(**kw)
+    model.load_state_dict(ref.state_dict(), strict=True)
+    sys.modules.pop(head, None)
+    model.eval()
+    x = torch.rand(2, 3 if head in ("pointnet_cls", "pose") else 10, 64)
+    a, b = ref(x), model(x)
+    for u, v in zip(a if isinstance(a, tuple) else (a,), b if isinstance(b, tuple) else (b,)):
+        np.testing.assert_array_equal(u.detach().numpy(), v.detach().numpy())
+    with pytest.raises(RuntimeError, match="ROCm device tensors only"):
+        with torch.no_grad():
+            model(x)
+
+
+# ---------------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", golden_names("v1_"))
+def test_v1_heads_match_reference_on_gpu(name):
+    from pn2 import _lib
+    g = load_golden("v1_%s.npz" % name)
+    model, _ = _build(name)
+    model = model.to("cuda").eval()
+    acts = {}
+    _hooks(model, acts)
+    with torch.no_grad():
+        out = model(*_args(g, "cuda"))
+    assert _lib.load().pn2_sa_mlp_last_path() == _lib.PATH_SPLIT_BF16
+    _check(g, out, acts, 1e-5, 1e-4)
+
+
+def _torch_layers(x_cf, convs, bns, relu_last=True):
+    h = x_cf
+    for i, (c, b) in enumerate(zip(convs, bns)):
+        h = b(c(h))
+        if relu_last or i < len(convs) - 1:
+            h = torch.relu(h)
+    return h
+
+
+def _rand_layers(cins, couts, seed):
+    torch.manual_seed(seed)
+    convs = [torch.nn.Conv1d(a, b, 1) for a, b in zip(cins, couts)]
+    bns = [torch.nn.BatchNorm1d(b) for b in couts]
+    for bn in bns:
+        cases.randomize_bn(bn, seed)
+    return [c.cuda().eval() for c in convs], [b.cuda().eval() for b in bns]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,N,cin,couts,pool,relu_last", [
+    (3, 1000, 64, [128, 1024], True, False),    # the encoder's conv2/conv3 (signed max)
+    (2, 777, 64, [64, 128, 1024], True, True),  # rotation.py layers 2-4 from rows
+    (2, 500, 128, [1024], True, False),
+    (4, 300, 64, [64], False, True),            # unpooled rows out
+    (1, 33, 64, [128, 256], False, False),      # unpooled, signed
+])
+def test_point_mlp_rows_source(B, N, cin, couts, pool, relu_last):
+    from pn2.pointnet_utils import point_mlp
+    convs, bns = _rand_layers([cin] + couts[:-1], couts, 11 + N)
+    rows = torch.randn(B, N, cin, device="cuda")
+    with torch.no_grad():
+        got = point_mlp(rows, convs, bns, {}, pool=pool, last_relu=relu_last)
+        ref = _torch_layers(rows.permute(0, 2, 1), convs, bns, relu_last)
+        ref = ref.max(2)[0] if pool else ref.permute(0, 2, 1)
+    assert_close(got.cpu().numpy(), ref.cpu().numpy(), 1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,N,pool", [(3, 1024, False), (10, 2048, True), (13, 100, True), (3, 5, False)])
+def test_point_mlp_channel_first_source(C, N, pool):
+    from pn2.pointnet_utils import point_mlp
+    convs, bns = _rand_layers([C], [64], 7 + C)
+    x = torch.randn(2, C, N, device="cuda")
+    with torch.no_grad():
+        got = point_mlp(x, convs, bns, {}, pool=pool)
+        ref = _torch_layers(x, convs, bns)
+        ref = ref.max(2)[0] if pool else ref.permute(0, 2, 1)
+    assert_close(got.cpu().numpy(), ref.cpu().numpy(), 1e-5)
