@@ -81,6 +81,8 @@ def parse():
                     help="graphed pipeline: keep the head on the compute stream")
     ap.add_argument("--slots", type=int, default=3,
                     help="graphed pipeline: batches in flight (geometry runs slots-1 ahead)")
+    ap.add_argument("--geometry-streams", type=int, default=2,
+                    help="graphed pipeline: 2 = consecutive batches' FPS chains on two streams")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="plain eager steps (default for single-head configs: pn2.pipeline)")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default=None,
@@ -208,7 +210,8 @@ def main():
         from pn2.pipeline import GraphedPipeline, PipelinedForward
         if not a.eager_pipeline:
             pf = GraphedPipeline(eager_models[0], geometry_cus=a.geometry_cus,
-                                 tail=not a.no_tail, nslots=a.slots)
+                                 tail=not a.no_tail, nslots=a.slots,
+                                 geometry_streams=a.geometry_streams)
         else:
             pf = PipelinedForward(eager_models[0], geometry_cus=a.geometry_cus,
                                   tail="auto" if a.tail else False)

@@ -48,6 +48,10 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
                                                  float *__restrict__ pts_packed, int cp) {
     constexpr int NW = NT / 64;
     static_assert(NW <= 16, "one 16-lane row reduces the wave slots");
+    // In the pipelined launch FPS shares every SIMD with the MLP kernels' waves, and its
+    // dependent chain (one short VALU burst, a reduction and a barrier per iteration) is the
+    // pipeline's critical path: its waves take issue priority over co-resident waves.
+    __builtin_amdgcn_s_setprio(3);
     constexpr int SLOT = (CM + 2 + 3) & ~3;  // {max, index, coords...} padded to 16 bytes
     const int C = FIXED ? CM : Crt;
     const int tid = threadIdx.x;

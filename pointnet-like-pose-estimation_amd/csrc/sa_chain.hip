@@ -102,6 +102,16 @@ __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const floa
 }
 
 
+// Materialise a split pair in registers at this point (see the layer-0 pre-pass loop): keeps
+// the compiler from sinking an epilogue to the pair's last use and holding its inputs live.
+template <int NP>
+__device__ __forceinline__ void pin_pair(Split &a, Split &b) {
+    if constexpr (NP == 3)
+        asm volatile("" : "+v"(a.h), "+v"(a.m), "+v"(a.l), "+v"(b.h), "+v"(b.m), "+v"(b.l));
+    else
+        asm volatile("" : "+v"(a.h), "+v"(b.h));
+}
+
 // ---- workgroup weight ring.  A step = one (tile, k-block) of a layer = its three 1 KB plane
 // fragments; every wave of the workgroup consumes the same steps in the same order (its own 32
 // rows), so one LDS copy of a step feeds all four waves' MFMAs (128 rows per 3 KB of weights --
@@ -154,7 +164,7 @@ __device__ __forceinline__ void stage_barrier() {
 // tile by tile from the ring like layers 1 and 2; KB0M == 0: layer 0 streams its input blocks
 // (k-outer, every output tile accumulating) with ordinary loads and the ring starts at layer 1.
 template <int T0, int T1, int KB0M, int NP>
-__global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_eu(2))) void sa_chain_kernel(
+__global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_eu(3))) void sa_chain_kernel(
     const ChainArgs A) {
     constexpr int kStepBytes = step_bytes<NP>(), kStageBytes = stage_bytes<NP>();
     extern __shared__ __attribute__((aligned(16))) char csm[];
@@ -318,6 +328,10 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             dep = __builtin_bit_cast(unsigned, __builtin_shufflevector(X1[2 * t].h, X1[2 * t].h, 0, 1));
 #pragma unroll
             for (int m = 0; m < 4; ++m) zc[m] = zn[m], uc[m] = un[m];
+            // Materialise tile t's split planes here: otherwise the epilogue of the last tile is
+            // sunk to its use at the end of layer 1, keeping its raw inputs (accumulator, BN
+            // scale / shift) live across layer 1 -- 24 VGPRs of spill at 2 waves/SIMD.
+            pin_pair<NP>(X1[2 * t], X1[2 * t + 1]);
         }
     } else if constexpr (KB0M > 0) {
         // ---- layer 0 from registers: the whole input gathered once (raw fp32), then k-outer
@@ -348,7 +362,10 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             }
         }
 #pragma unroll
-        for (int t = 0; t < T0; ++t) hidden_epilogue<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+        for (int t = 0; t < T0; ++t) {
+            hidden_epilogue<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+            pin_pair<NP>(X1[2 * t], X1[2 * t + 1]);
+        }
     } else {
         // ---- layer 0 streamed: k-outer, every output tile accumulating (transposed)
         cfloatx16 acc[T0];
@@ -371,7 +388,10 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int st = 0; st < kStages - 1; ++st) issue_stage(st);
 #pragma unroll
-        for (int t = 0; t < T0; ++t) hidden_epilogue<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+        for (int t = 0; t < T0; ++t) {
+            hidden_epilogue<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+            pin_pair<NP>(X1[2 * t], X1[2 * t + 1]);
+        }
     }
 
     // ---- layer 1: input in registers, k-outer (each input block dies after its use, so X1 and

@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must be loaded before libpn2.so: shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpn2.so")
+LIB_PATH = os.environ.get("PN2_LIB") or os.path.join(_HERE, "libpn2.so")  # PN2_LIB: A/B builds
 
 _i64 = ctypes.c_int64
 _int = ctypes.c_int

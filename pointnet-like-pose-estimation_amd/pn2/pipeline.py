@@ -45,6 +45,8 @@ stream when ``run`` is called.
 import atexit
 import ctypes
 
+import time
+
 import torch
 
 from . import _lib
@@ -113,6 +115,17 @@ def _streams(device, geometry_cus):
         ts, th = _masked_stream(device, geo, ncu)
         _partitions[key] = (gs, cs, ts, (gh, ch, th))
     return _partitions[key][:3]
+
+
+_geo2 = {}
+
+
+def _second_geometry_stream(device):
+    """Another high-priority stream for GraphedPipeline(geometry_streams=2) (shared CUs)."""
+    if device not in _geo2:
+        lo, hi = torch.cuda.Stream.priority_range()
+        _geo2[device] = torch.cuda.Stream(torch.device("cuda", device), priority=min(lo, hi))
+    return _geo2[device]
 
 
 def partition(device, geometry_cus):
@@ -270,17 +283,29 @@ class GraphedPipeline(PipelinedForward):
     them into the slot before its fps replay.  Outputs are cloned out of the static buffers on
     the stream that produced them, so they stay valid.
 
-    Measured (SSG B=32 N=1024, shared CUs): 69.5k-69.9k clouds/s, against 52.5k-67.6k for the
-    eager pipeline (host-bound: ~470 us of issue per batch vs ~210 us here,
-    tools/debug/host_cost.py).  Without the tail the head's dozen launches sit on the compute
-    stream (59.5k).
+    geometry_streams=2 (default, shared CUs): consecutive batches' geometry replays alternate
+    between two high-priority streams.  The FPS chain is latency-bound on 32 workgroups (one per
+    cloud) and, under contention with the MLP kernels, took ~377 us per SSG batch against the
+    compute stream's ~350 us -- the pipeline was geometry-bound (tools/debug/gpipe_events.py).
+    Two batches' chains in flight halve the geometry period; the compute stream is now the bound.
+
+    Measured (SSG B=32 N=1024, shared CUs): one geometry stream 72k-74k clouds/s, two 76.4k-77.7k
+    (against 52.5k-67.6k for the eager pipeline: host-bound, ~470 us of issue per batch vs ~210
+    us here, tools/debug/host_cost.py).  Without the tail the head's dozen launches sit on the
+    compute stream (59.5k).
     """
 
-    def __init__(self, model, geometry_cus=0, tail=True, nslots=3):
+    def __init__(self, model, geometry_cus=0, tail=True, nslots=3, geometry_streams=2):
         super().__init__(model, geometry_cus, bool(tail))
         if nslots < 2:
             raise ValueError("pn2.pipeline: GraphedPipeline needs at least 2 slots")
+        if geometry_cus > 0:
+            geometry_streams = 1  # the CU-partitioned geometry stream is one
+        if geometry_streams not in (1, 2):
+            raise ValueError("pn2.pipeline: geometry_streams is 1 or 2")
         self.nslots = int(nslots)
+        self.geometry_streams = int(geometry_streams)
+        self.trace = None
         self._key = None
         self._slots = None
 
@@ -368,23 +393,37 @@ class GraphedPipeline(PipelinedForward):
         if first == len(batches):
             return outs
         geo, main, tail = _streams(dev.index, self.geometry_cus)
+        geos = [geo] if self.geometry_streams == 1 else [geo, _second_geometry_stream(dev.index)]
         caller = torch.cuda.current_stream(dev)
-        for st in (geo, main, tail):
+        for st in geos + [main, tail]:
             st.wait_stream(caller)
         ns = self.nslots
         ev_fps, ev_sa, ev_head = [None] * ns, [None] * ns, [None] * ns
         starts = self._draw_all(len(batches) - first)
 
+        tr = self.trace  # optional list of per-batch timing events (tools/debug/gpipe_events.py)
+
+        def mark(j, name, stream):
+            if tr is not None:
+                while len(tr) <= j:
+                    tr.append({})
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(stream)
+                tr[j][name] = (e, time.perf_counter())
+
         def issue_fps(j):
             s = j % ns
             sl = self._slots[s]
+            geo = geos[j % len(geos)]
             with torch.cuda.stream(geo):
                 if ev_sa[s] is not None:  # batch j-ns is done with the slot's inputs
                     geo.wait_event(ev_sa[s])
+                mark(j, "geo0", geo)
                 sl.x.copy_(batches[j], non_blocking=True)
-                sl.start_buf.copy_(starts[j - first], non_blocking=True)
+                sl.start_buf.copy_(self._draw_row(starts, j - first), non_blocking=True)
                 sl.fps.replay()
                 ev_fps[s] = geo.record_event()
+                mark(j, "geo1", geo)
 
         with torch.no_grad():
             # the geometry runs ns-1 batches ahead of the compute stream
@@ -401,28 +440,37 @@ class GraphedPipeline(PipelinedForward):
                         main.wait_event(ev_head[s])
                     for d, e in zip(sl.extra, extra_of(i)):
                         d.copy_(e, non_blocking=True)
+                    mark(i, "sa0", main)
                     sl.sa.replay()
                     ev_sa[s] = main.record_event()
+                    mark(i, "sa1", main)
                 ts = tail if sl.head is not None else main
                 with torch.cuda.stream(ts):
                     if sl.head is not None:
                         ts.wait_event(ev_sa[s])
+                        mark(i, "hd0", ts)
                         sl.head.replay()
                     out = _clone(sl.out)
                     if post is not None:
                         out = post(i, out)
                     ev_head[s] = ts.record_event()
+                    mark(i, "hd1", ts)
                 outs.append(out)
+        for g in geos[1:]:
+            geo.wait_stream(g)
         self._pinned_evs[self._pinned_cur] = geo.record_event()  # uploads read it
         for st in (geo, main, tail):
             caller.wait_stream(st)
         return outs
 
     def _draw_all(self, k):
-        """Start draws of the next k batches, taken now in batch order then layer order (the
-        order k eager forwards take them), into rows of a pinned host buffer: one asynchronous
-        upload per batch, no per-draw pinning (hipHostMalloc) on the issue path.  Two buffers
-        alternate across calls; one is refilled once the uploads of the call before last ran."""
+        """The pinned host buffer that receives the start draws of the next k batches, one row
+        per batch (one asynchronous upload per batch, no per-draw pinning on the issue path).
+        Rows are drawn by ``_draw_row`` just before their batch's upload is issued -- in batch
+        order then layer order, the order k eager forwards take them -- so the host draws
+        overlap the GPU work of earlier batches instead of delaying the first launch.  Two
+        buffers alternate across calls; one is reused once the uploads of the call before last
+        ran."""
         shapes = [(B, N) for _, B, N in self._slots[0].starts]
         width = sum(B for B, _ in shapes)
         if not hasattr(self, "_pinned"):
@@ -434,9 +482,12 @@ class GraphedPipeline(PipelinedForward):
         if buf is None or buf.shape[0] < k or buf.shape[1] != width:
             buf = self._pinned[c] = torch.empty(max(k, 64), width, dtype=torch.long,
                                                 pin_memory=True)
-        for j in range(k):
-            off = 0
-            for B, N in shapes:
-                buf[j, off:off + B] = shard.draw_start(B, N, pin=False)
-                off += B
+        self._shapes = shapes
         return buf
+
+    def _draw_row(self, buf, j):
+        off = 0
+        for B, N in self._shapes:
+            buf[j, off:off + B] = shard.draw_start(B, N, pin=False)
+            off += B
+        return buf[j]
