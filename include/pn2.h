@@ -25,6 +25,10 @@
  *                                                            model/pointnet2_utils.py:150-156, 184-193
  *   pn2_sa_mlp_max_f32     grouped shared MLP (conv+bn+relu)* + max over the neighbourhood
  *                                                            model/pointnet2_utils.py:167-172, 211-218
+ *   pn2_prepare_points_f64 the scripts' input preparation: provider.normalization + torch.Tensor
+ *                          + provider.splice_torch + transpose (+ the translation heads' mean)
+ *                                                            provider.py:5-21, 166-180;
+ *                                                            test_translation.py:72-79
  */
 #ifndef PN2_H
 #define PN2_H
@@ -40,7 +44,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 4
+#define PN2_ABI_VERSION 5
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -186,19 +190,35 @@ int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers, int 
                         int pool, float *out, int64_t ostride, float *workspace,
                         int64_t workspace_bytes, void *stream);
 
+/* ---- input preparation (the step before the path) ----
+ * pts: a DataLoader batch as float64 [B,N,C] (np.loadtxt rows), element (b,n,c) at
+ * pts[b*sb + n*sn + c*sc].  For every cloud b, in float64 with numpy's operation order:
+ *   mean_out[b*C + c] (or NULL) = float32(np.mean(points[b, :3, c]))  -- the first 3 POINTS, as
+ *       test_translation.py:73 takes them, before normalising
+ *   normalize != 0: xyz' = (xyz - centroid) / max_n |xyz_n - centroid|  (provider.normalization:
+ *       centroid = sequential row sum / N, |v| = sqrt((x*x + y*y) + z*z)); C >= 3
+ *   out[(b*N + n)*(C+K) + c] = float32(xyz'_c) (c < 3), float32(p[c]) (3 <= c < C),
+ *       1.0f if c - C == labels[b] else 0.0f (C <= c < C+K, K = num_category; 0 = no splice)
+ * out is the [B,N,C+K] float32 storage whose transpose(2,1) view is the model input (the
+ * layout the reference's scripts hand the model).  labels: int64 [B] device, each in [0, K)
+ * (checked by the caller: the reference raises IndexError).  1 <= C <= 64. */
+int pn2_prepare_points_f64(const double *pts, int64_t B, int64_t N, int64_t C, int64_t sb,
+                           int64_t sn, int64_t sc, int normalize, const int64_t *labels,
+                           int64_t num_category, float *out, float *mean_out, void *stream);
+
 /* Which kernel family served this thread's last successful pn2_sa_mlp_max_* call:
  * PN2_PATH_F32 (fp32 MFMA kernels), PN2_PATH_SPLIT_BF16 (split-bf16 chain / dense kernels) or
  * PN2_PATH_BF16 (pn2_sa_mlp_max_bf16). */
+#define PN2_PATH_F32 1
+#define PN2_PATH_SPLIT_BF16 2
+#define PN2_PATH_BF16 3
+int pn2_sa_mlp_last_path(void);
+
 /* ---- runtime: CU-partitioned streams (pipelined serving, pn2/pipeline.py) ---- */
 int pn2_device_cu_count(int device, int *count);
 /* A stream whose kernels run only on the CUs set in mask (bit i of word i/32 = CU i). */
 int pn2_stream_create_cu_masked(int device, const uint32_t *mask, int mask_words, void **stream);
 int pn2_stream_destroy(void *stream);
-
-#define PN2_PATH_F32 1
-#define PN2_PATH_SPLIT_BF16 2
-#define PN2_PATH_BF16 3
-int pn2_sa_mlp_last_path(void);
 
 #ifdef __cplusplus
 }

@@ -166,3 +166,42 @@ def mlp_max_bf16(grouped, layers):
         y = (y - L["mean"]) * inv * L["gamma"] + L["beta"]
         x = np.maximum(y, 0.0).astype(np.float32)
     return x.max(axis=2).astype(np.float64)
+
+
+# ---------------------------------------------------------------------- input preparation
+def normalization(point_cloud):
+    """/root/reference/provider.py:5-21, restated with the same numpy calls (provider.py itself
+    imports open3d, absent here, so it cannot be imported): per cloud, centroid = np.mean over
+    points, centre, m = max of the Euclidean norms, divide.  float64 in, float64 out."""
+    B, N, C = point_cloud.shape
+    normalize = np.zeros((B, N, C))
+    for i in range(B):
+        pc = point_cloud[i]
+        centroid = np.mean(pc, axis=0)
+        pc = pc - centroid
+        m = np.max(np.sqrt(np.sum(pc ** 2, axis=1)))
+        pc = pc / m
+        normalize[i] = pc
+    return normalize
+
+
+def prepare_points(points, labels=None, num_category=7, with_mean=False, normalize=True):
+    """The scripts' preparation of a DataLoader batch (test_translation.py:72-79;
+    test_rotation.py:71-77 and test_classification.py:71-72 without the mean / splice):
+    float64 [B,N,C] numpy -> (float32 [B,N,C+K] storage of the model input, float32 mean [B,C]
+    or None).  splice_torch (provider.py:166-180) appends the one-hot as float32 channels."""
+    import torch
+    points = np.array(points, dtype=np.float64, copy=True)
+    mean = None
+    if with_mean:
+        mean = torch.Tensor(np.mean(points[:, :3, :], axis=1)).numpy()
+    if normalize:
+        points[:, :, 0:3] = normalization(points[:, :, 0:3])
+    pts = torch.Tensor(points)
+    if labels is not None and num_category:
+        B, N, _ = pts.shape
+        oh = torch.zeros(B, N, num_category)
+        for i in range(B):
+            oh[i, :, int(labels[i])] = 1
+        pts = torch.cat([pts, oh], 2)
+    return pts.numpy(), mean

@@ -71,6 +71,8 @@ SIGNATURES = {
     "pn2_device_cu_count": (_int, [_int, ctypes.POINTER(_int)]),
     "pn2_stream_create_cu_masked": (_int, [_int, ctypes.POINTER(ctypes.c_uint32), _int, ctypes.POINTER(_vp)]),
     "pn2_stream_destroy": (_int, [_vp]),
+    "pn2_prepare_points_f64": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _vp, _i64,
+                                      _vp, _vp, _vp]),
     "pn2_pack_layer_split_bf16": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp]),
     "pn2_sa_mlp_workspace_bytes": (_i64, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int]),
     "pn2_sa_mlp_max_f32": (_int, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int, _int, _vp,
@@ -80,7 +82,7 @@ SIGNATURES = {
                                    _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _lib = None
 
 

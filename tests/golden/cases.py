@@ -117,3 +117,28 @@ V1_CASES = {
                  'classify': True, 'num_category': 0, 'normal_channel': False,
                  'transform': True, 'feat_trans': True}),
 }
+
+
+def raw_batch(kind, B, N, seed, C=3):
+    """A float64 [B, N, C] batch as the DataLoader yields it (np.loadtxt rows: sensor points in
+    metres, off-centre, scale varying per cloud).  kind: 'raw', 'dup' (many exact duplicates,
+    as random_point_dropout leaves them), 'tiny' (a few points, one scale)."""
+    rng = np.random.default_rng(seed)
+    scale = rng.uniform(0.05, 2.0, (B, 1, 1))
+    off = rng.uniform(-3.0, 3.0, (B, 1, C))
+    x = rng.uniform(-1.0, 1.0, (B, N, C)) * scale + off
+    if kind == 'dup':
+        for b in range(B):
+            x[b, rng.random(N) < 0.6] = x[b, 0]
+    return x
+
+
+# input-preparation cases (provider.normalization + splice_torch + the translation mean):
+# name -> (kind, B, N, C, seed, with labels)
+PREP_CASES = {
+    'raw': ('raw', 4, 1024, 3, 400, True),
+    'dup': ('dup', 3, 2048, 3, 401, True),
+    'nolabel': ('raw', 2, 1000, 3, 402, False),
+    'c6': ('raw', 2, 512, 6, 403, True),
+    'tiny': ('tiny', 2, 2, 3, 404, True),
+}

@@ -13,6 +13,7 @@ Files:
                     seeded weights + BN statistics; the weights are regenerated from the seed
                     and pinned by a state_dict SHA-256)
   v1_<case>.npz     PointNet-v1 heads (cases.V1_CASES): encoder / T-Net / head outputs
+  prep_<case>.npz   input preparation (cases.PREP_CASES) by provider.py's own functions
 (`make_goldens.py v1` regenerates only the v1 files, etc.)
   meta.json         torch version, CPU capability, MKL/oneDNN versions, thread count
 """
@@ -142,6 +143,40 @@ def gen_v1(importlib):
         print("v1", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
 
 
+def _provider_functions():
+    """normalization / splice_torch from /root/reference/provider.py.  The module imports
+    open3d (absent here), so the two functions are compiled from its source text alone (read
+    only, nothing copied into the repository) and run with numpy / torch."""
+    import ast
+    src = open(os.path.join(os.path.dirname(REF_MODEL), "provider.py")).read()
+    tree = ast.parse(src)
+    keep = [n for n in tree.body if isinstance(n, ast.FunctionDef)
+            and n.name in ("normalization", "splice_torch")]
+    ns = {"np": np, "torch": torch}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), "provider.py", "exec"), ns)
+    return ns["normalization"], ns["splice_torch"]
+
+
+def gen_prep():
+    """The scripts' input preparation (test_translation.py:72-79) with the reference's own
+    provider functions: mean of the first 3 points, normalization, float32 cast, splice."""
+    normalization, splice_torch = _provider_functions()
+    for name, (kind, B, N, C, seed, with_labels) in cases.PREP_CASES.items():
+        raw = cases.raw_batch(kind, B, N, seed, C)
+        labels = torch.arange(B) % 7 if with_labels else None
+        points = raw.copy()
+        mean = torch.Tensor(np.mean(points[:, :3, :], axis=1))
+        points[:, :, 0:3] = normalization(points[:, :, 0:3])
+        points = torch.Tensor(points)
+        if labels is not None:
+            points = splice_torch(points, labels)
+        rec = {"raw": raw, "mean": mean.numpy(), "prepared": points.contiguous().numpy()}
+        if labels is not None:
+            rec["labels"] = labels.numpy()
+        np.savez_compressed(os.path.join(HERE, "prep_%s.npz" % name), **rec)
+        print("prep", name, {k: v.shape for k, v in rec.items()})
+
+
 def main():
     torch.set_num_threads(8)
     P, importlib = _ref()
@@ -152,6 +187,8 @@ def main():
         gen_heads(importlib)
     if not only or "v1" in only:
         gen_v1(importlib)
+    if not only or "prep" in only:
+        gen_prep()
     meta = {
         "torch": torch.__version__,
         "cpu_capability": torch.backends.cpu.get_cpu_capability(),
