@@ -76,3 +76,17 @@ def test_workspace_query(widths, cin, mode, fused):
         s.S, s.K = 1, 1024
     ws = L.pn2_sa_mlp_workspace_bytes(s, _layers(widths, cin), len(widths))
     assert (ws == 0) == fused and ws >= 0
+
+
+def test_io_library_exports_every_declared_symbol():
+    """libpn2io.so (the dataset text reader, host code) against include/pn2io.h."""
+    from pn2 import data
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "pn2io.h")).read(), flags=re.S)
+    syms = sorted(set(re.findall(r"\b(pn2io_[a-z0-9_]+)\s*\(", text)))
+    L = data.load()
+    assert len(syms) == 5
+    for s in syms:
+        assert hasattr(L, s), s
+    assert L.pn2io_abi_version() == data.ABI_VERSION
+    rc = L.pn2io_read_csv_f64(b"/nonexistent/x.txt", b",", 3, 10, None, None)
+    assert rc == -4 and b"bad argument" in L.pn2io_last_error()
