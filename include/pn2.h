@@ -25,6 +25,10 @@
  *                                                            model/pointnet2_utils.py:150-156, 184-193
  *   pn2_sa_mlp_max_f32     grouped shared MLP (conv+bn+relu)* + max over the neighbourhood
  *                                                            model/pointnet2_utils.py:167-172, 211-218
+ *   pn2_bn_train_stats_f32 / pn2_bn_relu_apply_f32 / pn2_group_max_f32 / pn2_bn_relu_backward_f32
+ *                          train-mode BatchNorm2d + ReLU + torch.max over K, forward and backward
+ *                                                            model/pointnet2_utils.py:167-172, 211-221
+ *                                                            (under autograd: train_rotation.py:99-133)
  *   pn2_prepare_points_f64 the scripts' input preparation: provider.normalization + torch.Tensor
  *                          + provider.splice_torch + transpose (+ the translation heads' mean)
  *                                                            provider.py:5-21, 166-180;
@@ -44,7 +48,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 5
+#define PN2_ABI_VERSION 6
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -205,6 +209,35 @@ int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers, int 
 int pn2_prepare_points_f64(const double *pts, int64_t B, int64_t N, int64_t C, int64_t sb,
                            int64_t sn, int64_t sc, int normalize, const int64_t *labels,
                            int64_t num_category, float *out, float *mean_out, void *stream);
+
+/* ---- training (batch-statistics BatchNorm) around library GEMMs; rows are channels-last
+ * [M][C] with row stride ld.  Workspace: pn2_bn_train_workspace_bytes(M, C) bytes (float64
+ * chunk partials), caller-owned. ----
+ * Column statistics of Y: mean, invstd = 1/sqrt(var_biased + eps); sxhat[c] = sum_r xhat
+ * (float64, for the conv bias gradient); when momentum > 0 also
+ * running_mean/var = (1-momentum)*old + momentum*(mean, var_unbiased) (torch's rule). */
+int64_t pn2_bn_train_workspace_bytes(int64_t M, int64_t C);
+int pn2_bn_train_stats_f32(const float *Y, int64_t M, int64_t C, int64_t ld, double eps,
+                           double momentum, float *running_mean, float *running_var, float *mean,
+                           float *invstd, double *sxhat, void *ws, int64_t ws_bytes, void *stream);
+/* A = relu((Y - mean) * invstd * gamma + beta). */
+int pn2_bn_relu_apply_f32(const float *Y, int64_t M, int64_t C, int64_t ld, const float *mean,
+                          const float *invstd, const float *gamma, const float *beta, float *A,
+                          int64_t lda, void *stream);
+/* out[g*ldo + c] = max over k < K of A[(g*K + k)*lda + c]; arg[g*C + c] = first argmax (int32). */
+int pn2_group_max_f32(const float *A, int64_t G, int64_t K, int64_t C, int64_t lda, float *out,
+                      int64_t ldo, int32_t *arg, void *stream);
+/* Backward of A = relu(bn_train(Y)): dXn = dA * [A > 0], with dA dense (ldd) or, when dA is
+ * NULL, scattered from the max: dA[r][c] = dOut[r/K][c] if arg[r/K][c] == r%K else 0.
+ * dbeta = sum_r dXn, dgamma = sum_r dXn*xhat (float64 sums), and
+ * dY = gamma*invstd*(dXn - dbeta/M - xhat*dgamma/M); dbias (or NULL) = sum_r dY, the preceding
+ * conv's bias gradient, from the forward's sxhat. */
+int pn2_bn_relu_backward_f32(const float *Y, int64_t M, int64_t C, int64_t ld, const float *mean,
+                             const float *invstd, const float *gamma, const float *beta,
+                             const float *dA, int64_t ldd, const float *dOut, int64_t ldo,
+                             const int32_t *arg, int64_t K, const double *sxhat, float *dY,
+                             int64_t ldy, float *dgamma, float *dbeta, float *dbias, void *ws,
+                             int64_t ws_bytes, void *stream);
 
 /* Which kernel family served this thread's last successful pn2_sa_mlp_max_* call:
  * PN2_PATH_F32 (fp32 MFMA kernels), PN2_PATH_SPLIT_BF16 (split-bf16 chain / dense kernels) or

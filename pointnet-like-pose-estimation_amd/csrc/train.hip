@@ -1,0 +1,341 @@
+// train.hip -- training-mode (batch-statistics) BatchNorm + ReLU + max over the neighbourhood,
+// forward and backward, for the SA layers' shared MLP.
+//
+// Reference: PointNetSetAbstraction.forward in train mode, /root/reference/model/
+// pointnet2_utils.py:167-172 (Conv2d 1x1 -> BatchNorm2d -> ReLU per layer, torch.max over the
+// K neighbours), the same for the MSG scales (:211-221); the loop train_rotation.py:99-133 runs
+// it under autograd.  BatchNorm2d in training normalises with the batch statistics over all
+// B*S*K rows (biased variance), updates running_mean / running_var (unbiased) with momentum, and
+// its backward couples every row of the batch through the two column sums below.
+//
+// The matmuls (Y = X W^T + b, dW = dY^T X, dX = dY W) are plain GEMMs and go to the library
+// (hipBLASLt via torch.mm, pn2/train.py); what is here is everything around them, fused so each
+// pass reads the [M, C] activations once:
+//   pn2_bn_train_stats_f32    column sum / sum of squares of Y (float64 partials per row chunk),
+//                             then mean, invstd, running-stat update
+//   pn2_bn_relu_apply_f32     A = relu((Y - mean) * invstd * gamma + beta)
+//   pn2_group_max_f32         out[g][c] = max_k A[g*K + k][c] and its first argmax
+//   pn2_bn_relu_backward_f32  dXn = dA * [A > 0] (dA from the next layer, or scattered from the
+//                             max: arg[g][c] == k ? dOut[g][c] : 0), its column sums
+//                             S1 = sum dXn and S2 = sum dXn * xhat (= dbeta, dgamma), then
+//                             dY = gamma * invstd * (dXn - S1/M - xhat * S2/M)
+// Layout: channels-last rows [M][C] with row stride ld (the SA path's layout), so every pass is
+// a coalesced column-tiled sweep: a 256-thread block covers 64 columns x 4 row lanes of one row
+// chunk and reduces through LDS; chunk partials are merged in float64 by a per-column pass.
+#include "pn2_internal.h"
+
+namespace pn2 {
+
+constexpr int kTrCols = 64;     // columns per block
+constexpr int kTrLanes = 4;     // row lanes per block
+constexpr int kTrChunk = 1024;  // rows per chunk (partials per chunk)
+constexpr int kTrUnroll = 8;    // rows in flight per thread in the column sweeps
+
+__device__ __forceinline__ float tr_xhat(float y, float mean, float invstd) { return (y - mean) * invstd; }
+
+// partial column sums of Y and Y^2 over row chunk blockIdx.y -> part[chunk][2][C] (double)
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float *__restrict__ Y, int64_t M,
+                                                               int64_t C, int64_t ld,
+                                                               double *__restrict__ part) {
+    __shared__ double red[2][kTrLanes][kTrCols];
+    const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
+    const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
+    const int64_t r0 = (int64_t)blockIdx.y * kTrChunk;
+    const int64_t r1 = r0 + kTrChunk < M ? r0 + kTrChunk : M;
+    double s = 0.0, q = 0.0;
+    if (c < C) {
+        // kTrUnroll rows in flight per thread: the loop is load-latency bound otherwise
+        int64_t r = r0 + ty;
+        for (; r + (kTrUnroll - 1) * kTrLanes < r1; r += kTrUnroll * kTrLanes) {
+            float v[kTrUnroll];
+#pragma unroll
+            for (int u = 0; u < kTrUnroll; ++u) v[u] = Y[(r + u * kTrLanes) * ld + c];
+#pragma unroll
+            for (int u = 0; u < kTrUnroll; ++u) s += (double)v[u], q += (double)v[u] * (double)v[u];
+        }
+        for (; r < r1; r += kTrLanes) {
+            const double y = (double)Y[r * ld + c];
+            s += y;
+            q += y * y;
+        }
+    }
+    red[0][ty][tx] = s;
+    red[1][ty][tx] = q;
+    __syncthreads();
+    if (ty == 0 && c < C) {
+        for (int l = 1; l < kTrLanes; ++l) s += red[0][l][tx], q += red[1][l][tx];
+        part[((int64_t)blockIdx.y * 2 + 0) * C + c] = s;
+        part[((int64_t)blockIdx.y * 2 + 1) * C + c] = q;
+    }
+}
+
+// merge the chunk partials of column c; mean, invstd; running-stat update (torch's BatchNorm
+// train-mode rule: biased variance normalises, unbiased variance enters running_var)
+// sum of the nch chunk partials of column c (pair p of the [chunk][2][C] layout), one wave per
+// column: each lane takes every 64th chunk, then a shuffle tree
+__device__ __forceinline__ double wave_col_sum(const double *__restrict__ part, int64_t nch, int64_t C,
+                                               int64_t c, int p) {
+    const int lane = threadIdx.x;
+    double s = 0.0;
+    for (int64_t k = lane; k < nch; k += 64) s += part[(k * 2 + p) * C + c];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    return s;
+}
+
+__global__ __launch_bounds__(64) void bn_stats_final_kernel(const double *__restrict__ part, int64_t nch,
+                                                            int64_t M, int64_t C, double eps,
+                                                            double momentum, float *running_mean,
+                                                            float *running_var,
+                                                            float *__restrict__ mean_out,
+                                                            float *__restrict__ invstd_out,
+                                                            double *__restrict__ sxhat) {
+    const int64_t c = blockIdx.x;
+    const double s = wave_col_sum(part, nch, C, c, 0), q = wave_col_sum(part, nch, C, c, 1);
+    if (threadIdx.x != 0) return;
+    const double mean = s / (double)M;
+    double var = q / (double)M - mean * mean;
+    if (var < 0.0) var = 0.0;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = (float)(1.0 / sqrt(var + eps));
+    // sum over rows of xhat = (y - mean_f32) * invstd_f32 with the rounded statistics the other
+    // kernels use: the conv bias gradient (sum of dY) is -gamma*invstd*dgamma/M times this
+    sxhat[c] = (s - (double)M * (double)mean_out[c]) * (double)invstd_out[c];
+    if (running_mean && momentum > 0.0) {
+        const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+        running_mean[c] = (float)((1.0 - momentum) * (double)running_mean[c] + momentum * mean);
+        running_var[c] = (float)((1.0 - momentum) * (double)running_var[c] + momentum * unb);
+    }
+}
+
+// elementwise sweeps: block (64 columns x 4 row lanes) walks kTrEwRows rows of its column tile
+constexpr int kTrEwRows = 64;
+
+__global__ __launch_bounds__(256) void bn_relu_apply_kernel(const float *__restrict__ Y, int64_t M,
+                                                            int64_t C, int64_t ld,
+                                                            const float *__restrict__ mean,
+                                                            const float *__restrict__ invstd,
+                                                            const float *__restrict__ gamma,
+                                                            const float *__restrict__ beta,
+                                                            float *__restrict__ A, int64_t lda) {
+    const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
+    const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
+    if (c >= C) return;
+    const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c];
+    const int64_t r0 = (int64_t)blockIdx.y * kTrEwRows;
+    const int64_t r1 = r0 + kTrEwRows < M ? r0 + kTrEwRows : M;
+#pragma unroll 4
+    for (int64_t r = r0 + ty; r < r1; r += kTrLanes) {
+        const float x = tr_xhat(Y[r * ld + c], mu, is) * ga + be;
+        A[r * lda + c] = x > 0.f ? x : 0.f;
+    }
+}
+
+// one thread per (group, column): max over the group's K rows, first index of the max
+__global__ __launch_bounds__(256) void group_max_kernel(const float *__restrict__ A, int64_t G,
+                                                        int64_t K, int64_t C, int64_t lda,
+                                                        float *__restrict__ out, int64_t ldo,
+                                                        int32_t *__restrict__ arg) {
+    const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
+    const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
+    const int64_t g = (int64_t)blockIdx.y * kTrLanes + ty;
+    if (c >= C || g >= G) return;
+    const float *p = A + g * K * lda + c;
+    float m = p[0];
+    int32_t a = 0;
+    int64_t k = 1;
+    for (; k + 8 <= K; k += 8) {  // 8 rows in flight
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[(k + u) * lda];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (v[u] > m || (v[u] != v[u] && m == m)) m = v[u], a = (int32_t)(k + u);  // NaN wins
+    }
+    for (; k < K; ++k) {
+        const float v = p[k * lda];
+        if (v > m || (v != v && m == m)) m = v, a = (int32_t)k;  // NaN wins, as torch.max
+    }
+    out[g * ldo + c] = m;
+    arg[g * C + c] = a;
+}
+
+// dXn of row r, column c (see header); dA dense [M][C] (ldd) or scattered from the max
+__device__ __forceinline__ float tr_dxn(const float *__restrict__ Y, int64_t ld, int64_t r, int64_t c,
+                                        float mean, float invstd, float gamma, float beta,
+                                        const float *__restrict__ dA, int64_t ldd,
+                                        const float *__restrict__ dOut, int64_t ldo,
+                                        const int32_t *__restrict__ arg, int64_t K, int64_t C,
+                                        float &xhat) {
+    // branch-free: every load is issued whatever the ReLU mask, so unrolled rows stay in flight
+    xhat = tr_xhat(Y[r * ld + c], mean, invstd);
+    float d;
+    if (dA) {
+        d = dA[r * ldd + c];
+    } else {
+        const int64_t g = r / K;
+        const float o = dOut[g * ldo + c];
+        d = arg[g * C + c] == (int32_t)(r - g * K) ? o : 0.f;
+    }
+    return xhat * gamma + beta > 0.f ? d : 0.f;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
+    const float *__restrict__ Y, int64_t M, int64_t C, int64_t ld, const float *__restrict__ mean,
+    const float *__restrict__ invstd, const float *__restrict__ gamma, const float *__restrict__ beta,
+    const float *__restrict__ dA, int64_t ldd, const float *__restrict__ dOut, int64_t ldo,
+    const int32_t *__restrict__ arg, int64_t K, double *__restrict__ part) {
+    __shared__ double red[2][kTrLanes][kTrCols];
+    const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
+    const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
+    const int64_t r0 = (int64_t)blockIdx.y * kTrChunk;
+    const int64_t r1 = r0 + kTrChunk < M ? r0 + kTrChunk : M;
+    double s1 = 0.0, s2 = 0.0;
+    if (c < C) {
+        const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c];
+        int64_t r = r0 + ty;
+        for (; r + (kTrUnroll - 1) * kTrLanes < r1; r += kTrUnroll * kTrLanes) {
+            float d[kTrUnroll], xh[kTrUnroll];
+#pragma unroll
+            for (int u = 0; u < kTrUnroll; ++u)
+                d[u] = tr_dxn(Y, ld, r + u * kTrLanes, c, mu, is, ga, be, dA, ldd, dOut, ldo, arg, K, C, xh[u]);
+#pragma unroll
+            for (int u = 0; u < kTrUnroll; ++u) s1 += (double)d[u], s2 += (double)d[u] * (double)xh[u];
+        }
+        for (; r < r1; r += kTrLanes) {
+            float xh;
+            const float d = tr_dxn(Y, ld, r, c, mu, is, ga, be, dA, ldd, dOut, ldo, arg, K, C, xh);
+            s1 += (double)d;
+            s2 += (double)d * (double)xh;
+        }
+    }
+    red[0][ty][tx] = s1;
+    red[1][ty][tx] = s2;
+    __syncthreads();
+    if (ty == 0 && c < C) {
+        for (int l = 1; l < kTrLanes; ++l) s1 += red[0][l][tx], s2 += red[1][l][tx];
+        part[((int64_t)blockIdx.y * 2 + 0) * C + c] = s1;
+        part[((int64_t)blockIdx.y * 2 + 1) * C + c] = s2;
+    }
+}
+
+__global__ __launch_bounds__(64) void bn_bwd_final_kernel(const double *__restrict__ part, int64_t nch,
+                                                          int64_t M, int64_t C, const float *__restrict__ gamma,
+                                                          const float *__restrict__ invstd,
+                                                          const double *__restrict__ sxhat,
+                                                          float *__restrict__ dbeta, float *__restrict__ dgamma,
+                                                          float *__restrict__ dbias, double *__restrict__ sums) {
+    const int64_t c = blockIdx.x;
+    const double s1 = wave_col_sum(part, nch, C, c, 0), s2 = wave_col_sum(part, nch, C, c, 1);
+    if (threadIdx.x != 0) return;
+    dbeta[c] = (float)s1;
+    dgamma[c] = (float)s2;
+    sums[c] = s1;
+    sums[C + c] = s2;
+    // sum_r dY = gamma*invstd*(s1 - M*(s1/M) - (s2/M)*sum_r xhat): the conv bias gradient
+    if (dbias) dbias[c] = (float)(-(double)gamma[c] * (double)invstd[c] * (s2 / (double)M) * sxhat[c]);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const float *__restrict__ Y, int64_t M, int64_t C, int64_t ld, const float *__restrict__ mean,
+    const float *__restrict__ invstd, const float *__restrict__ gamma, const float *__restrict__ beta,
+    const float *__restrict__ dA, int64_t ldd, const float *__restrict__ dOut, int64_t ldo,
+    const int32_t *__restrict__ arg, int64_t K, const double *__restrict__ sums,
+    float *__restrict__ dY, int64_t ldy) {
+    const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
+    const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
+    if (c >= C) return;
+    const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c];
+    const float m1 = (float)(sums[c] / (double)M), m2 = (float)(sums[C + c] / (double)M);
+    const int64_t r0 = (int64_t)blockIdx.y * kTrEwRows;
+    const int64_t r1 = r0 + kTrEwRows < M ? r0 + kTrEwRows : M;
+#pragma unroll 4
+    for (int64_t r = r0 + ty; r < r1; r += kTrLanes) {
+        float xh;
+        const float d = tr_dxn(Y, ld, r, c, mu, is, ga, be, dA, ldd, dOut, ldo, arg, K, C, xh);
+        dY[r * ldy + c] = ga * is * (d - m1 - xh * m2);
+    }
+}
+
+inline int64_t chunks(int64_t M) { return (M + kTrChunk - 1) / kTrChunk; }
+
+}  // namespace pn2
+
+using namespace pn2;
+
+extern "C" int64_t pn2_bn_train_workspace_bytes(int64_t M, int64_t C) {
+    if (M <= 0 || C <= 0) return 0;
+    return chunks(M) * 2 * C * (int64_t)sizeof(double) + 3 * C * (int64_t)sizeof(double);
+}
+
+extern "C" int pn2_bn_train_stats_f32(const float *Y, int64_t M, int64_t C, int64_t ld, double eps,
+                                      double momentum, float *running_mean, float *running_var,
+                                      float *mean, float *invstd, double *sxhat, void *ws,
+                                      int64_t ws_bytes, void *stream) {
+    PN2_REQUIRE(Y && mean && invstd && sxhat && ws, "pn2_bn_train_stats_f32: null pointer");
+    PN2_REQUIRE(M >= 1 && C >= 1 && ld >= C, "pn2_bn_train_stats_f32: bad shape");
+    PN2_REQUIRE(ws_bytes >= pn2_bn_train_workspace_bytes(M, C), "pn2_bn_train_stats_f32: workspace too small");
+    PN2_REQUIRE(momentum <= 0.0 || (running_mean && running_var), "pn2_bn_train_stats_f32: running stats");
+    hipStream_t st = as_stream(stream);
+    double *part = static_cast<double *>(ws);
+    hipLaunchKernelGGL(bn_stats_partial_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)chunks(M)),
+                       dim3(256), 0, st, Y, M, C, ld, part);
+    PN2_LAUNCH_CHECK("bn_stats_partial_kernel");
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((unsigned)C), dim3(64), 0, st, part, chunks(M), M, C,
+                       eps, momentum, running_mean, running_var, mean, invstd, sxhat);
+    PN2_LAUNCH_CHECK("bn_stats_final_kernel");
+    return PN2_OK;
+}
+
+extern "C" int pn2_bn_relu_apply_f32(const float *Y, int64_t M, int64_t C, int64_t ld, const float *mean,
+                                     const float *invstd, const float *gamma, const float *beta, float *A,
+                                     int64_t lda, void *stream) {
+    PN2_REQUIRE(Y && mean && invstd && gamma && beta && A, "pn2_bn_relu_apply_f32: null pointer");
+    PN2_REQUIRE(M >= 0 && C >= 1 && ld >= C && lda >= C, "pn2_bn_relu_apply_f32: bad shape");
+    if (M == 0) return PN2_OK;
+    hipLaunchKernelGGL(bn_relu_apply_kernel,
+                       dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)((M + kTrEwRows - 1) / kTrEwRows)),
+                       dim3(256), 0, as_stream(stream), Y, M, C, ld, mean, invstd, gamma, beta, A, lda);
+    PN2_LAUNCH_CHECK("bn_relu_apply_kernel");
+    return PN2_OK;
+}
+
+extern "C" int pn2_group_max_f32(const float *A, int64_t G, int64_t K, int64_t C, int64_t lda, float *out,
+                                 int64_t ldo, int32_t *arg, void *stream) {
+    PN2_REQUIRE(A && out && arg, "pn2_group_max_f32: null pointer");
+    PN2_REQUIRE(G >= 0 && K >= 1 && C >= 1 && lda >= C && ldo >= C, "pn2_group_max_f32: bad shape");
+    if (G == 0) return PN2_OK;
+    hipLaunchKernelGGL(group_max_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)((G + kTrLanes - 1) / kTrLanes)),
+                       dim3(256), 0, as_stream(stream), A, G, K, C, lda, out, ldo, arg);
+    PN2_LAUNCH_CHECK("group_max_kernel");
+    return PN2_OK;
+}
+
+extern "C" int pn2_bn_relu_backward_f32(const float *Y, int64_t M, int64_t C, int64_t ld, const float *mean,
+                                        const float *invstd, const float *gamma, const float *beta,
+                                        const float *dA, int64_t ldd, const float *dOut, int64_t ldo,
+                                        const int32_t *arg, int64_t K, const double *sxhat,
+                                        float *dY, int64_t ldy, float *dgamma, float *dbeta,
+                                        float *dbias, void *ws, int64_t ws_bytes, void *stream) {
+    PN2_REQUIRE(Y && mean && invstd && gamma && beta && dY && dgamma && dbeta && ws && (!dbias || sxhat),
+                "pn2_bn_relu_backward_f32: null pointer");
+    PN2_REQUIRE(dA || (dOut && arg && K >= 1 && M % K == 0), "pn2_bn_relu_backward_f32: need dA or (dOut, arg, K)");
+    PN2_REQUIRE(M >= 1 && C >= 1 && ld >= C && ldy >= C && (!dA || ldd >= C) && (dA || ldo >= C),
+                "pn2_bn_relu_backward_f32: bad shape");
+    PN2_REQUIRE(ws_bytes >= pn2_bn_train_workspace_bytes(M, C), "pn2_bn_relu_backward_f32: workspace too small");
+    hipStream_t st = as_stream(stream);
+    double *part = static_cast<double *>(ws);
+    double *sums = part + chunks(M) * 2 * C;
+    hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)chunks(M)),
+                       dim3(256), 0, st, Y, M, C, ld, mean, invstd, gamma, beta, dA, ldd, dOut, ldo, arg, K, part);
+    PN2_LAUNCH_CHECK("bn_bwd_partial_kernel");
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((unsigned)C), dim3(64), 0, st, part, chunks(M), M, C, gamma,
+                       invstd, sxhat, dbeta, dgamma, dbias, sums);
+    PN2_LAUNCH_CHECK("bn_bwd_final_kernel");
+    hipLaunchKernelGGL(bn_bwd_apply_kernel,
+                       dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)((M + kTrEwRows - 1) / kTrEwRows)),
+                       dim3(256), 0, st, Y, M, C, ld, mean, invstd, gamma, beta, dA, ldd, dOut, ldo, arg, K,
+                       sums, dY, ldy);
+    PN2_LAUNCH_CHECK("bn_bwd_apply_kernel");
+    return PN2_OK;
+}

@@ -71,6 +71,14 @@ SIGNATURES = {
     "pn2_device_cu_count": (_int, [_int, ctypes.POINTER(_int)]),
     "pn2_stream_create_cu_masked": (_int, [_int, ctypes.POINTER(ctypes.c_uint32), _int, ctypes.POINTER(_vp)]),
     "pn2_stream_destroy": (_int, [_vp]),
+    "pn2_bn_train_workspace_bytes": (_i64, [_i64, _i64]),
+    "pn2_bn_train_stats_f32": (_int, [_vp, _i64, _i64, _i64, ctypes.c_double, ctypes.c_double, _vp,
+                                      _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "pn2_bn_relu_apply_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "pn2_group_max_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp]),
+    "pn2_bn_relu_backward_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                        _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64,
+                                        _vp]),
     "pn2_prepare_points_f64": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _vp, _i64,
                                       _vp, _vp, _vp]),
     "pn2_pack_layer_split_bf16": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp]),
@@ -82,7 +90,7 @@ SIGNATURES = {
                                    _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _lib = None
 
 

@@ -16,8 +16,9 @@ MLP):
 
 Training (``model.train()`` or autograd through the weights) keeps the reference's semantics
 (batch-statistics BatchNorm, autograd through the MLP and the feature gather): FPS and the ball
-query still run as HIP kernels (they are index ops with no gradient), the differentiable part
-runs as torch device ops.
+query still run as HIP kernels (they are index ops with no gradient); in train mode the
+grouping and the MLP + max run forward and backward on the training kernels of pn2/train.py
+(csrc/train.hip around library GEMMs); eval with autograd uses torch device ops.
 
 Device tensors only -- the reference's CPU execution is not re-implemented here.
 """
@@ -29,6 +30,7 @@ from . import _lib
 from . import geometry
 from . import ops
 from . import shard
+from . import train
 
 
 # ----------------------------------------------------------------------------- helpers
@@ -90,7 +92,12 @@ def _pack_chain(convs, bns, cache, rot0, xyz=0, xyz_first=True):
 
 
 def _torch_group(points, idx, centers, feature, feature_first):
-    """Differentiable grouping for the training path (torch device gathers)."""
+    """Differentiable grouping for the training path: the HIP grouping kernel with an
+    index_add_ backward for the features (pn2/train.py), or torch device gathers when the
+    coordinates need a gradient too."""
+    g = train.group_train(points, idx, centers, feature, feature_first)
+    if g is not None:
+        return g
     B = points.shape[0]
     b = torch.arange(B, device=points.device).view(B, 1, 1)
     g = points[b, idx, :] - centers.unsqueeze(2)
@@ -101,6 +108,11 @@ def _torch_group(points, idx, centers, feature, feature_first):
 
 
 def _torch_mlp_max(grouped, convs, bns):
+    """grouped [B,S,K,C] -> [B, Cout, S].  Training on the device: the fused batch-statistics
+    BN / ReLU / max kernels around library GEMMs (pn2/train.py); otherwise (eval with autograd,
+    exotic BN configs) the reference's torch formulation."""
+    if train.eligible(grouped, convs, bns):
+        return train.mlp_max_train(grouped, convs, bns)
     x = grouped.permute(0, 3, 2, 1)  # [B, C, K, S] as the reference (:167)
     for conv, bn in zip(convs, bns):
         x = F.relu(bn(conv(x)))

@@ -142,3 +142,24 @@ PREP_CASES = {
     'c6': ('raw', 2, 512, 6, 403, True),
     'tiny': ('tiny', 2, 2, 3, 404, True),
 }
+
+
+# training-mode SA layers: name -> (kind: 'ssg' | 'msg', ctor args, B, N,
+# feature channels D, weight seed, forward seed)
+TRAIN_CASES = {
+    'ssg_xyz': ('ssg', (64, 32, 0.4, 3, [32, 32, 64], False), 2, 512, 0, 500, 600),
+    'ssg_feat': ('ssg', (32, 16, 0.5, 3 + 16, [32, 64], False), 2, 256, 16, 501, 601),
+    'group_all': ('ssg', (None, None, None, 3 + 32, [64, 128], True), 3, 128, 32, 502, 602),
+    'msg': ('msg', (32, [8, 16], [0.3, 0.6], 16, [[16, 32], [32, 32]]), 2, 256, 16, 503, 603),
+}
+
+
+def train_inputs(B, N, D, seed):
+    """points [B, 3, N] (unit-sphere cloud, channel-first), feature [B, D, N] or None, and the
+    loss weights R are drawn by the caller once the output shape is known."""
+    pts = cloud('uniform3', B, N, seed).permute(0, 2, 1).contiguous()
+    feat = None
+    if D:
+        g = torch.Generator().manual_seed(seed + 1)
+        feat = torch.randn(B, D, N, generator=g)
+    return pts, feat

@@ -14,6 +14,7 @@ Files:
                     and pinned by a state_dict SHA-256)
   v1_<case>.npz     PointNet-v1 heads (cases.V1_CASES): encoder / T-Net / head outputs
   prep_<case>.npz   input preparation (cases.PREP_CASES) by provider.py's own functions
+  train_<case>.npz  training-mode SA forward + backward (cases.TRAIN_CASES)
 (`make_goldens.py v1` regenerates only the v1 files, etc.)
   meta.json         torch version, CPU capability, MKL/oneDNN versions, thread count
 """
@@ -177,6 +178,37 @@ def gen_prep():
         print("prep", name, {k: v.shape for k, v in rec.items()})
 
 
+def gen_train(P):
+    """Training-mode forward + backward of SA layers with the reference modules: outputs,
+    parameter / feature gradients of loss = sum(out_feature * R), running statistics after."""
+    for name, (kind, args, B, N, D, wseed, fseed) in cases.TRAIN_CASES.items():
+        ctor = P.PointNetSetAbstraction if kind == 'ssg' else P.PointNetSetAbstractionMsg
+        torch.manual_seed(wseed)
+        mod = ctor(*args)
+        cases.randomize_bn(mod, wseed + 1)
+        mod.train()
+        pts, feat = cases.train_inputs(B, N, D, wseed + 2)
+        rec = {"points": pts.numpy(), "state_hash": np.array(cases.state_hash(mod))}
+        if feat is not None:
+            rec["feature"] = feat.numpy()
+            feat = feat.clone().requires_grad_(True)
+        torch.manual_seed(fseed)
+        new_points, new_feature = mod(pts, feat)
+        R = torch.randn(new_feature.shape, generator=torch.Generator().manual_seed(wseed + 3))
+        (new_feature * R).sum().backward()
+        rec["new_points"] = new_points.detach().numpy()
+        rec["new_feature"] = new_feature.detach().numpy()
+        rec["R"] = R.numpy()
+        if feat is not None:
+            rec["feature_grad"] = feat.grad.numpy()
+        for k, p in mod.named_parameters():
+            rec["grad." + k] = p.grad.numpy()
+        for k, b in mod.named_buffers():
+            rec["buf." + k] = b.numpy()
+        np.savez_compressed(os.path.join(HERE, "train_%s.npz" % name), **rec)
+        print("train", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
+
+
 def main():
     torch.set_num_threads(8)
     P, importlib = _ref()
@@ -189,6 +221,8 @@ def main():
         gen_v1(importlib)
     if not only or "prep" in only:
         gen_prep()
+    if not only or "train" in only:
+        gen_train(P)
     meta = {
         "torch": torch.__version__,
         "cpu_capability": torch.backends.cpu.get_cpu_capability(),
