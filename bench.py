@@ -204,23 +204,32 @@ def main():
 
     # single-head configs run software-pipelined (pn2.pipeline: the FPS chain of step i+1 on
     # its own CUs while step i's MLPs run); same kernels, results and RNG draws as eager steps
-    pipelined = len(eager_models) == 1 and not a.graph and not a.no_pipeline
+    pipelined = not a.graph and not a.no_pipeline
     pf = None
     if pipelined:
-        from pn2.pipeline import GraphedPipeline, PipelinedForward
+        from pn2.pipeline import GraphedPipeline, MultiHead, PipelinedForward
+        # several heads (config pose): one module, heads in step()'s order, so the FPS draws
+        # come in the same order and every head's geometry overlaps every head's MLPs
+        pmodel = eager_models[0] if len(eager_models) == 1 else MultiHead(
+            eager_models, [i for i, n in enumerate(names) if n.startswith("translation")])
         if not a.eager_pipeline:
-            pf = GraphedPipeline(eager_models[0], geometry_cus=a.geometry_cus,
+            pf = GraphedPipeline(pmodel, geometry_cus=a.geometry_cus,
                                  tail=not a.no_tail, nslots=a.slots,
                                  geometry_streams=a.geometry_streams)
         else:
-            pf = PipelinedForward(eager_models[0], geometry_cus=a.geometry_cus,
+            pf = PipelinedForward(pmodel, geometry_cus=a.geometry_cus,
                                   tail="auto" if a.tail else False)
+
+    takes_mean = any(n.startswith("translation") for n in names)
+
+    def gather(i, o):  # step()'s all_gather of every head's first output
+        if len(names) > 1:
+            return [shard.all_gather_rows(h[0] if isinstance(h, tuple) else h) for h in o]
+        return shard.all_gather_rows(o[0] if isinstance(o, tuple) else o)
 
     def run_pipelined(k):
         with shard.batch_shard(gB, lo):
-            pf.run([x] * k, None if mean is None or not names[0].startswith("translation")
-                   else [(mean,)] * k,
-                   post=lambda i, o: shard.all_gather_rows(o[0] if isinstance(o, tuple) else o))
+            pf.run([x] * k, [(mean,)] * k if takes_mean else None, post=gather)
 
     for _ in range(max(a.warmup, 2) if a.graph else a.warmup):  # graph: 1st call captures
         step(names, models, x, mean, gB, lo)

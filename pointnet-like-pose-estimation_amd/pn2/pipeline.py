@@ -117,15 +117,16 @@ def _streams(device, geometry_cus):
     return _partitions[key][:3]
 
 
-_geo2 = {}
+_geo_extra = {}
 
 
-def _second_geometry_stream(device):
-    """Another high-priority stream for GraphedPipeline(geometry_streams=2) (shared CUs)."""
-    if device not in _geo2:
-        lo, hi = torch.cuda.Stream.priority_range()
-        _geo2[device] = torch.cuda.Stream(torch.device("cuda", device), priority=min(lo, hi))
-    return _geo2[device]
+def _extra_geometry_streams(device, n):
+    """n more high-priority streams for GraphedPipeline(geometry_streams=1+n) (shared CUs)."""
+    have = _geo_extra.setdefault(device, [])
+    lo, hi = torch.cuda.Stream.priority_range()
+    while len(have) < n:
+        have.append(torch.cuda.Stream(torch.device("cuda", device), priority=min(lo, hi)))
+    return have[:n]
 
 
 def partition(device, geometry_cus):
@@ -165,12 +166,15 @@ class PipelinedForward:
     def _fps_chain(self, x):
         """Geometry of every SA layer for input x ([B, C, N]): FPS (draws in layer order) and
         the ball query of each radius -- both read only coordinates, so a batch's whole
-        geometry runs ahead of its MLPs."""
+        geometry runs ahead of its MLPs.  A group_all layer ends a head's chain; an SA layer
+        after it starts the next head's chain from the input again (a model holding several
+        heads over the same cloud, e.g. MultiHead(rotation_ssg, translation_ssg))."""
         entries = {}
         pts = x.permute(0, 2, 1)
         for sa in self.sas:
             if getattr(sa, "group_all", False):
-                break
+                pts = x.permute(0, 2, 1)
+                continue
             B, N, C = pts.shape
             _, newp, cpk, ppk = ops.fps_direct(pts, sa.point_number, shard.device_start(B, N, x.device))
             if isinstance(sa, PointNetSetAbstractionMsg):
@@ -239,6 +243,23 @@ class PipelinedForward:
                 outs.append(out)
 
 
+class MultiHead(torch.nn.Module):
+    """Several heads over the same input as one module, so the pipeline overlaps all of their
+    geometry with all of their MLPs: forward(x, *extras) -> tuple of each head's output, the
+    heads called in order (their FPS draws in that order, as separate eager calls take them).
+    extra_heads: indices of the heads that also take the extras (translation heads' mean)."""
+
+    def __init__(self, heads, extra_heads=()):
+        super().__init__()
+        self.heads = torch.nn.ModuleList(heads)
+        self.extra_heads = set(extra_heads)
+        self.training = any(h.training for h in heads)  # the heads' mode, unchanged
+
+    def forward(self, x, *extras):
+        return tuple(h(x, *extras) if i in self.extra_heads else h(x)
+                     for i, h in enumerate(self.heads))
+
+
 def _clone(o):
     if isinstance(o, torch.Tensor):
         return o.clone()
@@ -301,6 +322,9 @@ class GraphedPipeline(PipelinedForward):
             raise ValueError("pn2.pipeline: GraphedPipeline needs at least 2 slots")
         if geometry_cus > 0:
             geometry_streams = 1  # the CU-partitioned geometry stream is one
+        # 2 at most: with the compute and tail streams that is the 4 hardware queues a process
+        # gets (GPU_MAX_HW_QUEUES); a fifth stream shares a queue and serialises behind another
+        # (measured: 3 geometry streams 42.8k clouds/s at SSG vs 76.1k with 2)
         if geometry_streams not in (1, 2):
             raise ValueError("pn2.pipeline: geometry_streams is 1 or 2")
         self.nslots = int(nslots)
@@ -393,7 +417,7 @@ class GraphedPipeline(PipelinedForward):
         if first == len(batches):
             return outs
         geo, main, tail = _streams(dev.index, self.geometry_cus)
-        geos = [geo] if self.geometry_streams == 1 else [geo, _second_geometry_stream(dev.index)]
+        geos = [geo] + _extra_geometry_streams(dev.index, self.geometry_streams - 1)
         caller = torch.cuda.current_stream(dev)
         for st in geos + [main, tail]:
             st.wait_stream(caller)

@@ -380,3 +380,34 @@ def test_graphed_pipeline_matches_eager(head, tail):
     for g, w in zip(got2, want2):
         for a, b in zip(g, w):
             np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * float(np.abs(b).max()))
+
+
+def test_graphed_pipeline_multihead_matches_eager():
+    """BASELINE config 4 (rotation_ssg + translation_ssg over the same clouds) as one
+    pn2.pipeline.MultiHead: the FPS chain covers both heads (a group_all layer ends a head's
+    chain, the next head restarts from the input), draws in the order separate eager calls take
+    them, and every output matches those calls (logits to 1e-6: head BLAS on another stream)."""
+    from pn2 import heads as H
+    from pn2 import shard
+    from pn2.pipeline import GraphedPipeline, MultiHead
+    torch.manual_seed(12)
+    rot, tra = H.RotationSSG().eval(), H.TranslationSSG().eval()
+    cases.randomize_bn(rot, 12)
+    cases.randomize_bn(tra, 13)
+    rot, tra = rot.to(DEV), tra.to(DEV)
+    B, N = 8, 2048
+    xs = [cases.cloud("onehot10", B, N, 70 + i).permute(0, 2, 1).contiguous().to(DEV) for i in range(5)]
+    means = [(torch.randn(B, 3, generator=torch.Generator().manual_seed(i)).to(DEV),) for i in range(5)]
+    torch.manual_seed(41)
+    with torch.no_grad(), shard.batch_shard(4 * B, 2 * B):
+        want = [(rot(x).cpu().numpy(), tra(x, *m).cpu().numpy()) for x, m in zip(xs, means)]
+    rng_want = torch.randint(0, 1 << 30, (4,))
+    gp = GraphedPipeline(MultiHead([rot, tra], [1]))
+    torch.manual_seed(41)
+    with shard.batch_shard(4 * B, 2 * B):
+        got = [tuple(t.cpu().numpy() for t in o) for o in gp.run(xs, means)]
+    np.testing.assert_array_equal(torch.randint(0, 1 << 30, (4,)).numpy(), rng_want.numpy())
+    for i, (g, w) in enumerate(zip(got, want)):
+        for k, (a, b) in enumerate(zip(g, w)):
+            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * float(np.abs(b).max()),
+                                       err_msg="head %d of batch %d" % (k, i))
