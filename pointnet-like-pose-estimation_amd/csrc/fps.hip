@@ -108,6 +108,34 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
     }
     if (LDSC && tid < 3) key[tid] = 0ull;
 
+    // ---- channels past xyz that are constant over the cloud (the pose heads' one-hot class:
+    // one label per cloud) contribute (v - v)^2 = +0 to every distance, and adding +0 leaves
+    // each of the reference's channel-sum orders equal to ((dx^2 + dy^2) + dz^2) -- so such a
+    // cloud runs the 3-channel loop, bit-identically.  Non-finite constants keep the full
+    // loop (inf - inf is NaN).
+    bool cst = true;
+    if constexpr (FIXED && CM > 3) {
+#pragma unroll
+        for (int k = 3; k < CM; ++k) {
+            const float v0 = P[(int64_t)k * sc];
+            cst = cst && __builtin_isfinite(v0);
+#pragma unroll
+            for (int j = 0; j < 2 * PH; ++j)
+                if (j < PPT && tid * PPT + j < N) cst = cst && (q[j >> 1][k][j & 1] == v0);
+        }
+    }
+    // block AND through a spare LDS word behind the key words (no static LDS: the cloud copy
+    // may use the whole 160 KB dynamically)
+    bool xyz_only = false;
+    if constexpr (FIXED && CM > 3) {
+        int *flag = reinterpret_cast<int *>(fsm + ((S + 3) & ~3) + 6);
+        if (tid == 0) *flag = 1;
+        __syncthreads();
+        if (!cst) *flag = 0;  // every writer stores 0: a benign race
+        __syncthreads();
+        xyz_only = *flag != 0;
+    }
+
     // ---- serial loop
     int far = (int)start[b];
     float c[CM];
@@ -122,15 +150,25 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
         // distances (two points per packed op) and the running min -- branchless
 #pragma unroll
         for (int h = 0; h < PH; ++h) {
-            pn2_f2 sq[CM];
-#pragma unroll
-            for (int k = 0; k < CM; ++k) {
-                const pn2_f2 d = q[h][k] - c[k];
-                sq[k] = d * d;
-            }
             pn2_f2 dd;
-            if constexpr (FIXED && CM == 3) dd = seq_sum<CM>(sq, C);  // every rule agrees for C=3
-            else dd = layout_sum<CM>(sq, C, rule[h]);
+            if (xyz_only) {
+                pn2_f2 s3[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const pn2_f2 d = q[h][k] - c[k];
+                    s3[k] = d * d;
+                }
+                dd = (s3[0] + s3[1]) + s3[2];
+            } else {
+                pn2_f2 sq[CM];
+#pragma unroll
+                for (int k = 0; k < CM; ++k) {
+                    const pn2_f2 d = q[h][k] - c[k];
+                    sq[k] = d * d;
+                }
+                if constexpr (FIXED && CM == 3) dd = seq_sum<CM>(sq, C);  // every rule agrees for C=3
+                else dd = layout_sum<CM>(sq, C, rule[h]);
+            }
             // strict '<' update == min on the (non-negative) float bits; padding stays 0
             dist[2 * h] = min(dist[2 * h], __float_as_uint(dd.x));
             if (2 * h + 1 < PPT) dist[2 * h + 1] = min(dist[2 * h + 1], __float_as_uint(dd.y));
