@@ -56,6 +56,8 @@ CONFIGS = {
     "pose": ("rotation_ssg+translation_ssg", 8, 2048, "onehot10",
              "rotation_ssg + translation_ssg forward, B=8/GPU (64 on 8 GPUs), N=2048, 10-ch"),
     "stress": ("pointnet2_cls_ssg", 128, 16384, "uniform3", "pointnet2_cls_ssg forward, B=128/GPU, N=16384"),
+    # BASELINE config 1 (the reference runs it on the CPU): PointNet-v1 on the v1 kernels
+    "v1": ("pointnet_cls", 8, 1024, "uniform3", "pointnet_cls (PointNet v1) forward, B=8/GPU, N=1024"),
 }
 # MLP arithmetic per config: BASELINE config 5 (stress) asks for features/MLP in bf16, the
 # others are the reference's fp32
@@ -96,11 +98,12 @@ def build_models(cfg, dev):
     import cases
     from pn2 import heads
     head = CONFIGS[cfg][0]
+    from pn2 import heads_v1
     names = head.split("+")
     models = []
     for i, n in enumerate(names):
         torch.manual_seed(1000 + i)
-        m = heads.HEADS[n]()
+        m = heads.HEADS[n]() if n in heads.HEADS else heads_v1.HEADS_V1[n]()
         cases.randomize_bn(m, 2000 + i)
         models.append(m.eval().to(dev))
     return names, models
@@ -198,6 +201,11 @@ def main():
     lo, hi = shard.shard_range(gB, rank, world)
     names, eager_models = build_models(a.config, dev)
     from pn2.graphs import GraphedForward
+    from pn2.pipeline import PointNetSetAbstraction, PointNetSetAbstractionMsg
+    has_sa = any(isinstance(mod, (PointNetSetAbstraction, PointNetSetAbstractionMsg))
+                 for m in eager_models for mod in m.modules())
+    if not has_sa and not a.no_pipeline:
+        a.graph = True  # v1: no FPS chain to overlap; whole-forward HIP-graph replay instead
     models = [GraphedForward(m) for m in eager_models] if a.graph else eager_models
     x, mean = make_inputs(a.config, hi - lo, lo, dev, rank)
     torch.manual_seed(1234)  # identical CPU RNG stream on every rank (FPS start draws)

@@ -123,6 +123,11 @@ class _TNet(nn.Module):
         self.bn5 = nn.BatchNorm1d(256)
         self._k = k
         self._cache = {}
+        # the reference rebuilds eye(k) from numpy and copies it to the device every forward
+        # (pointnet_utils.py:37-40); here it is a non-persistent buffer (state_dict unchanged)
+        # that moves with the module, so the forward has no host copy and captures in a graph
+        self.register_buffer("_iden", torch.from_numpy(np.eye(k).flatten().astype(np.float32)).view(1, k * k),
+                             persistent=False)
 
     def forward(self, x):
         """x: [B, C, N] (any strides: a rows view is read as rows, not copied)."""
@@ -139,9 +144,7 @@ class _TNet(nn.Module):
         g = F.relu(self.bn4(self.fc1(g)))
         g = F.relu(self.bn5(self.fc2(g)))
         g = self.fc3(g)
-        iden = torch.from_numpy(np.eye(self._k).flatten().astype(np.float32)).view(
-            1, self._k * self._k).repeat(B, 1)
-        g = g + iden.to(g.device)
+        g = g + self._iden.expand(B, -1)
         return g.view(-1, self._k, self._k)
 
 
