@@ -38,6 +38,9 @@ __device__ __forceinline__ unsigned row_max_u32(unsigned v) {
 
 // LDSC: keep a copy of the cloud in LDS (N*CM floats) so the winner's coordinates are one
 // broadcast ds_read; otherwise they travel with the per-wave slots.
+#ifndef PN2_FPS_PRIO
+#define PN2_FPS_PRIO 3
+#endif
 template <int NT, int PPT, int CM, bool FIXED, bool LDSC>
 __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, int N, int Crt,
                                                  int64_t sb, int64_t sn, int64_t sc, int kind,
@@ -51,7 +54,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
     // In the pipelined launch FPS shares every SIMD with the MLP kernels' waves, and its
     // dependent chain (one short VALU burst, a reduction and a barrier per iteration) is the
     // pipeline's critical path: its waves take issue priority over co-resident waves.
-    __builtin_amdgcn_s_setprio(3);
+    __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
     constexpr int SLOT = (CM + 2 + 3) & ~3;  // {max, index, coords...} padded to 16 bytes
     const int C = FIXED ? CM : Crt;
     const int tid = threadIdx.x;
