@@ -25,10 +25,13 @@
  *                                                            model/pointnet2_utils.py:150-156, 184-193
  *   pn2_sa_mlp_max_f32     grouped shared MLP (conv+bn+relu)* + max over the neighbourhood
  *                                                            model/pointnet2_utils.py:167-172, 211-218
- *   pn2_bn_train_stats_f32 / pn2_bn_relu_apply_f32 / pn2_group_max_f32 / pn2_bn_relu_backward_f32
+ *   pn2_bn_train_stats_f32 / pn2_bn_relu_apply_f32 (/ pn2_bn_train_forward_f32: both) /
+ *   pn2_group_max_f32 / pn2_bn_relu_backward_f32
  *                          train-mode BatchNorm2d + ReLU + torch.max over K, forward and backward
  *                                                            model/pointnet2_utils.py:167-172, 211-221
  *                                                            (under autograd: train_rotation.py:99-133)
+ *                          and the v1 shared MLPs' Conv1d + BatchNorm1d (+ ReLU) + max over N
+ *                                                            model/pointnet_utils.py:31-35, 118-128
  *   pn2_prepare_points_f64 the scripts' input preparation: provider.normalization + torch.Tensor
  *                          + provider.splice_torch + transpose (+ the translation heads' mean)
  *                                                            provider.py:5-21, 166-180;
@@ -48,7 +51,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 6
+#define PN2_ABI_VERSION 7
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -133,7 +136,9 @@ typedef struct pn2_mlp_layer {
 
 /* Layer without the ReLU: out = alpha * (W x) + beta (PointNetEncoder's conv3 + bn3 before its
  * max, /root/reference/model/pointnet_utils.py:125-127).  Served by the split dense-layer
- * kernels only (group_all / rows sources); other kernels reject it with PN2_EUNSUPPORTED. */
+ * kernels only (group_all / rows sources); other kernels reject it with PN2_EUNSUPPORTED.  The
+ * training entry points (pn2_bn_relu_apply_f32 / pn2_bn_relu_backward_f32) take it as their
+ * flags argument. */
 #define PN2_LAYER_NO_RELU 1
 
 /* The same W packed for the split-bf16 chain kernel: three bf16 planes (hi, mid, lo with
@@ -220,14 +225,22 @@ int64_t pn2_bn_train_workspace_bytes(int64_t M, int64_t C);
 int pn2_bn_train_stats_f32(const float *Y, int64_t M, int64_t C, int64_t ld, double eps,
                            double momentum, float *running_mean, float *running_var, float *mean,
                            float *invstd, double *sxhat, void *ws, int64_t ws_bytes, void *stream);
-/* A = relu((Y - mean) * invstd * gamma + beta). */
+/* A = relu((Y - mean) * invstd * gamma + beta); flags PN2_LAYER_NO_RELU: no ReLU. */
 int pn2_bn_relu_apply_f32(const float *Y, int64_t M, int64_t C, int64_t ld, const float *mean,
                           const float *invstd, const float *gamma, const float *beta, float *A,
-                          int64_t lda, void *stream);
-/* out[g*ldo + c] = max over k < K of A[(g*K + k)*lda + c]; arg[g*C + c] = first argmax (int32). */
+                          int64_t lda, int flags, void *stream);
+/* pn2_bn_train_stats_f32 then pn2_bn_relu_apply_f32 in one call (one host crossing per layer):
+ * stats = [mean | invstd], 2*C floats. */
+int pn2_bn_train_forward_f32(const float *Y, int64_t M, int64_t C, int64_t ld, double eps,
+                             double momentum, float *running_mean, float *running_var,
+                             const float *gamma, const float *beta, float *A, int64_t lda, int flags,
+                             float *stats, double *sxhat, void *ws, int64_t ws_bytes, void *stream);
+/* out[g*ldo + c] = max over k < K of A[(g*K + k)*lda + c]; arg[g*C + c] = first argmax (int32);
+ * NaN is the maximum (first NaN), as torch.max. */
 int pn2_group_max_f32(const float *A, int64_t G, int64_t K, int64_t C, int64_t lda, float *out,
                       int64_t ldo, int32_t *arg, void *stream);
-/* Backward of A = relu(bn_train(Y)): dXn = dA * [A > 0], with dA dense (ldd) or, when dA is
+/* Backward of A = relu(bn_train(Y)): dXn = dA * [A > 0] (dA with flags PN2_LAYER_NO_RELU, the
+ * backward of A = bn_train(Y)), with dA dense (ldd) or, when dA is
  * NULL, scattered from the max: dA[r][c] = dOut[r/K][c] if arg[r/K][c] == r%K else 0.
  * dbeta = sum_r dXn, dgamma = sum_r dXn*xhat (float64 sums), and
  * dY = gamma*invstd*(dXn - dbeta/M - xhat*dgamma/M); dbias (or NULL) = sum_r dY, the preceding
@@ -237,7 +250,7 @@ int pn2_bn_relu_backward_f32(const float *Y, int64_t M, int64_t C, int64_t ld, c
                              const float *dA, int64_t ldd, const float *dOut, int64_t ldo,
                              const int32_t *arg, int64_t K, const double *sxhat, float *dY,
                              int64_t ldy, float *dgamma, float *dbeta, float *dbias, void *ws,
-                             int64_t ws_bytes, void *stream);
+                             int64_t ws_bytes, int flags, void *stream);
 
 /* Which kernel family served this thread's last successful pn2_sa_mlp_max_* call:
  * PN2_PATH_F32 (fp32 MFMA kernels), PN2_PATH_SPLIT_BF16 (split-bf16 chain / dense kernels) or

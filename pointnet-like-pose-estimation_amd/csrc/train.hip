@@ -13,10 +13,12 @@
 // pass reads the [M, C] activations once:
 //   pn2_bn_train_stats_f32    column sum / sum of squares of Y (float64 partials per row chunk),
 //                             then mean, invstd, running-stat update
-//   pn2_bn_relu_apply_f32     A = relu((Y - mean) * invstd * gamma + beta)
+//   pn2_bn_relu_apply_f32     A = relu((Y - mean) * invstd * gamma + beta)  (no ReLU with
+//                             PN2_LAYER_NO_RELU: PointNet-v1's conv3 + bn3 before its max)
 //   pn2_group_max_f32         out[g][c] = max_k A[g*K + k][c] and its first argmax
-//   pn2_bn_relu_backward_f32  dXn = dA * [A > 0] (dA from the next layer, or scattered from the
-//                             max: arg[g][c] == k ? dOut[g][c] : 0), its column sums
+//   pn2_bn_relu_backward_f32  dXn = dA * [A > 0] (unmasked with PN2_LAYER_NO_RELU; dA from the
+//                             next layer, or scattered from the max: arg[g][c] == k ?
+//                             dOut[g][c] : 0), its column sums
 //                             S1 = sum dXn and S2 = sum dXn * xhat (= dbeta, dgamma), then
 //                             dY = gamma * invstd * (dXn - S1/M - xhat * S2/M)
 // Layout: channels-last rows [M][C] with row stride ld (the SA path's layout), so every pass is
@@ -28,20 +30,22 @@ namespace pn2 {
 
 constexpr int kTrCols = 64;     // columns per block
 constexpr int kTrLanes = 4;     // row lanes per block
-constexpr int kTrChunk = 1024;  // rows per chunk (partials per chunk)
+constexpr int kTrChunk = 1024;  // rows per chunk (partials per chunk), at most
+constexpr int kTrChunkMin = 64;
+constexpr int kTrMinBlocks = 2048;  // column sweeps: enough blocks to fill 256 CUs several times
 constexpr int kTrUnroll = 8;    // rows in flight per thread in the column sweeps
 
 __device__ __forceinline__ float tr_xhat(float y, float mean, float invstd) { return (y - mean) * invstd; }
 
 // partial column sums of Y and Y^2 over row chunk blockIdx.y -> part[chunk][2][C] (double)
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const float *__restrict__ Y, int64_t M,
-                                                               int64_t C, int64_t ld,
+                                                               int64_t C, int64_t ld, int64_t chunk,
                                                                double *__restrict__ part) {
     __shared__ double red[2][kTrLanes][kTrCols];
     const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
     const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
-    const int64_t r0 = (int64_t)blockIdx.y * kTrChunk;
-    const int64_t r1 = r0 + kTrChunk < M ? r0 + kTrChunk : M;
+    const int64_t r0 = (int64_t)blockIdx.y * chunk;
+    const int64_t r1 = r0 + chunk < M ? r0 + chunk : M;
     double s = 0.0, q = 0.0;
     if (c < C) {
         // kTrUnroll rows in flight per thread: the loop is load-latency bound otherwise
@@ -117,7 +121,8 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(const float *__restr
                                                             const float *__restrict__ invstd,
                                                             const float *__restrict__ gamma,
                                                             const float *__restrict__ beta,
-                                                            float *__restrict__ A, int64_t lda) {
+                                                            float *__restrict__ A, int64_t lda,
+                                                            int relu) {
     const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
     const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
     if (c >= C) return;
@@ -127,7 +132,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(const float *__restr
 #pragma unroll 4
     for (int64_t r = r0 + ty; r < r1; r += kTrLanes) {
         const float x = tr_xhat(Y[r * ld + c], mu, is) * ga + be;
-        A[r * lda + c] = x > 0.f ? x : 0.f;
+        A[r * lda + c] = relu ? (x > 0.f ? x : 0.f) : x;  // relu is uniform: no divergence
     }
 }
 
@@ -160,36 +165,89 @@ __global__ __launch_bounds__(256) void group_max_kernel(const float *__restrict_
     arg[g * C + c] = a;
 }
 
+// (v, a) beats (m, b) in the max's order: NaN above every number, then value, then the first
+// index (torch.max's first argmax)
+__device__ __forceinline__ bool tr_better(float v, int32_t a, float m, int32_t b) {
+    if (v != v) return m == m || a < b;
+    if (m != m) return false;
+    return v > m || (v == m && a < b);
+}
+
+// Large K (a PointNet-v1 max over a cloud's N points): one block per (group, 64 columns), the K
+// rows split over kTrWideLanes row lanes (8 rows in flight each), lanes merged through LDS.
+// One thread per (group, column) walking all K rows would serialise K/8 dependent load rounds.
+constexpr int kTrWideLanes = 16;
+constexpr int kTrWideK = 256;  // K from which the wide kernel is used
+
+__global__ __launch_bounds__(kTrCols * kTrWideLanes) void group_max_wide_kernel(
+    const float *__restrict__ A, int64_t K, int64_t C, int64_t lda, float *__restrict__ out, int64_t ldo,
+    int32_t *__restrict__ arg) {
+    __shared__ float sv[kTrWideLanes][kTrCols];
+    __shared__ int32_t sa[kTrWideLanes][kTrCols];
+    const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
+    const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
+    const int64_t g = blockIdx.y;
+    float m = -__builtin_inff();
+    int32_t a = 0x7fffffff;
+    if (c < C) {
+        const float *p = A + g * K * lda + c;
+        int64_t k = ty;
+        for (; k + 7 * kTrWideLanes < K; k += 8 * kTrWideLanes) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = p[(k + u * kTrWideLanes) * lda];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)  // increasing row order within the lane: strict > keeps the first
+                if (v[u] > m || (v[u] != v[u] && m == m) || a == 0x7fffffff)
+                    m = v[u], a = (int32_t)(k + u * kTrWideLanes);
+        }
+        for (; k < K; k += kTrWideLanes) {
+            const float v = p[k * lda];
+            if (v > m || (v != v && m == m) || a == 0x7fffffff) m = v, a = (int32_t)k;
+        }
+    }
+    sv[ty][tx] = m;
+    sa[ty][tx] = a;
+    __syncthreads();
+    if (ty == 0 && c < C) {
+        for (int l = 1; l < kTrWideLanes; ++l)
+            if (sa[l][tx] != 0x7fffffff && tr_better(sv[l][tx], sa[l][tx], m, a)) m = sv[l][tx], a = sa[l][tx];
+        out[g * ldo + c] = m;
+        arg[g * C + c] = a;
+    }
+}
+
 // dXn of row r, column c (see header); dA dense [M][C] (ldd) or scattered from the max
 __device__ __forceinline__ float tr_dxn(const float *__restrict__ Y, int64_t ld, int64_t r, int64_t c,
                                         float mean, float invstd, float gamma, float beta,
                                         const float *__restrict__ dA, int64_t ldd,
                                         const float *__restrict__ dOut, int64_t ldo,
                                         const int32_t *__restrict__ arg, int64_t K, int64_t C,
-                                        float &xhat) {
+                                        int relu, float &xhat) {
     // branch-free: every load is issued whatever the ReLU mask, so unrolled rows stay in flight
     xhat = tr_xhat(Y[r * ld + c], mean, invstd);
     float d;
     if (dA) {
         d = dA[r * ldd + c];
     } else {
-        const int64_t g = r / K;
-        const float o = dOut[g * ldo + c];
-        d = arg[g * C + c] == (int32_t)(r - g * K) ? o : 0.f;
+        // 32-bit division (the host checks M < 2^31): the 64-bit one is a long call sequence
+        const uint32_t g = (uint32_t)r / (uint32_t)K;
+        const float o = dOut[(int64_t)g * ldo + c];
+        d = arg[(int64_t)g * C + c] == (int32_t)((uint32_t)r - g * (uint32_t)K) ? o : 0.f;
     }
-    return xhat * gamma + beta > 0.f ? d : 0.f;
+    return !relu || xhat * gamma + beta > 0.f ? d : 0.f;
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     const float *__restrict__ Y, int64_t M, int64_t C, int64_t ld, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma, const float *__restrict__ beta,
     const float *__restrict__ dA, int64_t ldd, const float *__restrict__ dOut, int64_t ldo,
-    const int32_t *__restrict__ arg, int64_t K, double *__restrict__ part) {
+    const int32_t *__restrict__ arg, int64_t K, int relu, int64_t chunk, double *__restrict__ part) {
     __shared__ double red[2][kTrLanes][kTrCols];
     const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
     const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
-    const int64_t r0 = (int64_t)blockIdx.y * kTrChunk;
-    const int64_t r1 = r0 + kTrChunk < M ? r0 + kTrChunk : M;
+    const int64_t r0 = (int64_t)blockIdx.y * chunk;
+    const int64_t r1 = r0 + chunk < M ? r0 + chunk : M;
     double s1 = 0.0, s2 = 0.0;
     if (c < C) {
         const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c];
@@ -198,13 +256,13 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
             float d[kTrUnroll], xh[kTrUnroll];
 #pragma unroll
             for (int u = 0; u < kTrUnroll; ++u)
-                d[u] = tr_dxn(Y, ld, r + u * kTrLanes, c, mu, is, ga, be, dA, ldd, dOut, ldo, arg, K, C, xh[u]);
+                d[u] = tr_dxn(Y, ld, r + u * kTrLanes, c, mu, is, ga, be, dA, ldd, dOut, ldo, arg, K, C, relu, xh[u]);
 #pragma unroll
             for (int u = 0; u < kTrUnroll; ++u) s1 += (double)d[u], s2 += (double)d[u] * (double)xh[u];
         }
         for (; r < r1; r += kTrLanes) {
             float xh;
-            const float d = tr_dxn(Y, ld, r, c, mu, is, ga, be, dA, ldd, dOut, ldo, arg, K, C, xh);
+            const float d = tr_dxn(Y, ld, r, c, mu, is, ga, be, dA, ldd, dOut, ldo, arg, K, C, relu, xh);
             s1 += (double)d;
             s2 += (double)d * (double)xh;
         }
@@ -240,7 +298,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const float *__restrict__ Y, int64_t M, int64_t C, int64_t ld, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ gamma, const float *__restrict__ beta,
     const float *__restrict__ dA, int64_t ldd, const float *__restrict__ dOut, int64_t ldo,
-    const int32_t *__restrict__ arg, int64_t K, const double *__restrict__ sums,
+    const int32_t *__restrict__ arg, int64_t K, int relu, const double *__restrict__ sums,
     float *__restrict__ dY, int64_t ldy) {
     const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
     const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
@@ -252,12 +310,21 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 #pragma unroll 4
     for (int64_t r = r0 + ty; r < r1; r += kTrLanes) {
         float xh;
-        const float d = tr_dxn(Y, ld, r, c, mu, is, ga, be, dA, ldd, dOut, ldo, arg, K, C, xh);
+        const float d = tr_dxn(Y, ld, r, c, mu, is, ga, be, dA, ldd, dOut, ldo, arg, K, C, relu, xh);
         dY[r * ldy + c] = ga * is * (d - m1 - xh * m2);
     }
 }
 
-inline int64_t chunks(int64_t M) { return (M + kTrChunk - 1) / kTrChunk; }
+// rows per partial chunk of the column sweeps: kTrChunk, halved while the grid (column tiles x
+// chunks) would have fewer than kTrMinBlocks blocks -- PointNet-v1 layers have M = B*N = 32k
+// rows (32 chunks of 1024: a 64-column layer would run on 32 workgroups), SA layers 500k
+inline int64_t chunk_rows(int64_t M, int64_t C) {
+    const int64_t tiles = (C + kTrCols - 1) / kTrCols;
+    int64_t ch = kTrChunk;
+    while (ch > kTrChunkMin && tiles * ((M + ch - 1) / ch) < kTrMinBlocks) ch >>= 1;
+    return ch;
+}
+inline int64_t chunks(int64_t M, int64_t C) { const int64_t ch = chunk_rows(M, C); return (M + ch - 1) / ch; }
 
 }  // namespace pn2
 
@@ -265,7 +332,7 @@ using namespace pn2;
 
 extern "C" int64_t pn2_bn_train_workspace_bytes(int64_t M, int64_t C) {
     if (M <= 0 || C <= 0) return 0;
-    return chunks(M) * 2 * C * (int64_t)sizeof(double) + 3 * C * (int64_t)sizeof(double);
+    return chunks(M, C) * 2 * C * (int64_t)sizeof(double) + 3 * C * (int64_t)sizeof(double);
 }
 
 extern "C" int pn2_bn_train_stats_f32(const float *Y, int64_t M, int64_t C, int64_t ld, double eps,
@@ -278,10 +345,10 @@ extern "C" int pn2_bn_train_stats_f32(const float *Y, int64_t M, int64_t C, int6
     PN2_REQUIRE(momentum <= 0.0 || (running_mean && running_var), "pn2_bn_train_stats_f32: running stats");
     hipStream_t st = as_stream(stream);
     double *part = static_cast<double *>(ws);
-    hipLaunchKernelGGL(bn_stats_partial_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)chunks(M)),
-                       dim3(256), 0, st, Y, M, C, ld, part);
+    hipLaunchKernelGGL(bn_stats_partial_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)chunks(M, C)),
+                       dim3(256), 0, st, Y, M, C, ld, chunk_rows(M, C), part);
     PN2_LAUNCH_CHECK("bn_stats_partial_kernel");
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((unsigned)C), dim3(64), 0, st, part, chunks(M), M, C,
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((unsigned)C), dim3(64), 0, st, part, chunks(M, C), M, C,
                        eps, momentum, running_mean, running_var, mean, invstd, sxhat);
     PN2_LAUNCH_CHECK("bn_stats_final_kernel");
     return PN2_OK;
@@ -289,22 +356,43 @@ extern "C" int pn2_bn_train_stats_f32(const float *Y, int64_t M, int64_t C, int6
 
 extern "C" int pn2_bn_relu_apply_f32(const float *Y, int64_t M, int64_t C, int64_t ld, const float *mean,
                                      const float *invstd, const float *gamma, const float *beta, float *A,
-                                     int64_t lda, void *stream) {
+                                     int64_t lda, int flags, void *stream) {
     PN2_REQUIRE(Y && mean && invstd && gamma && beta && A, "pn2_bn_relu_apply_f32: null pointer");
     PN2_REQUIRE(M >= 0 && C >= 1 && ld >= C && lda >= C, "pn2_bn_relu_apply_f32: bad shape");
+    PN2_REQUIRE((flags & ~PN2_LAYER_NO_RELU) == 0, "pn2_bn_relu_apply_f32: unknown flags");
     if (M == 0) return PN2_OK;
     hipLaunchKernelGGL(bn_relu_apply_kernel,
                        dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)((M + kTrEwRows - 1) / kTrEwRows)),
-                       dim3(256), 0, as_stream(stream), Y, M, C, ld, mean, invstd, gamma, beta, A, lda);
+                       dim3(256), 0, as_stream(stream), Y, M, C, ld, mean, invstd, gamma, beta, A, lda,
+                       (flags & PN2_LAYER_NO_RELU) ? 0 : 1);
     PN2_LAUNCH_CHECK("bn_relu_apply_kernel");
     return PN2_OK;
+}
+
+extern "C" int pn2_bn_train_forward_f32(const float *Y, int64_t M, int64_t C, int64_t ld, double eps,
+                                        double momentum, float *running_mean, float *running_var,
+                                        const float *gamma, const float *beta, float *A, int64_t lda,
+                                        int flags, float *stats, double *sxhat, void *ws, int64_t ws_bytes,
+                                        void *stream) {
+    PN2_REQUIRE(stats, "pn2_bn_train_forward_f32: null pointer");
+    const int rc = pn2_bn_train_stats_f32(Y, M, C, ld, eps, momentum, running_mean, running_var, stats,
+                                          stats + C, sxhat, ws, ws_bytes, stream);
+    if (rc != PN2_OK) return rc;
+    return pn2_bn_relu_apply_f32(Y, M, C, ld, stats, stats + C, gamma, beta, A, lda, flags, stream);
 }
 
 extern "C" int pn2_group_max_f32(const float *A, int64_t G, int64_t K, int64_t C, int64_t lda, float *out,
                                  int64_t ldo, int32_t *arg, void *stream) {
     PN2_REQUIRE(A && out && arg, "pn2_group_max_f32: null pointer");
-    PN2_REQUIRE(G >= 0 && K >= 1 && C >= 1 && lda >= C && ldo >= C, "pn2_group_max_f32: bad shape");
+    PN2_REQUIRE(G >= 0 && K >= 1 && K < ((int64_t)1 << 31) && C >= 1 && lda >= C && ldo >= C,
+                "pn2_group_max_f32: bad shape");
     if (G == 0) return PN2_OK;
+    if (K >= kTrWideK && G < 65536) {
+        hipLaunchKernelGGL(group_max_wide_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)G),
+                           dim3(kTrCols * kTrWideLanes), 0, as_stream(stream), A, K, C, lda, out, ldo, arg);
+        PN2_LAUNCH_CHECK("group_max_wide_kernel");
+        return PN2_OK;
+    }
     hipLaunchKernelGGL(group_max_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)((G + kTrLanes - 1) / kTrLanes)),
                        dim3(256), 0, as_stream(stream), A, G, K, C, lda, out, ldo, arg);
     PN2_LAUNCH_CHECK("group_max_kernel");
@@ -316,26 +404,30 @@ extern "C" int pn2_bn_relu_backward_f32(const float *Y, int64_t M, int64_t C, in
                                         const float *dA, int64_t ldd, const float *dOut, int64_t ldo,
                                         const int32_t *arg, int64_t K, const double *sxhat,
                                         float *dY, int64_t ldy, float *dgamma, float *dbeta,
-                                        float *dbias, void *ws, int64_t ws_bytes, void *stream) {
+                                        float *dbias, void *ws, int64_t ws_bytes, int flags, void *stream) {
     PN2_REQUIRE(Y && mean && invstd && gamma && beta && dY && dgamma && dbeta && ws && (!dbias || sxhat),
                 "pn2_bn_relu_backward_f32: null pointer");
     PN2_REQUIRE(dA || (dOut && arg && K >= 1 && M % K == 0), "pn2_bn_relu_backward_f32: need dA or (dOut, arg, K)");
-    PN2_REQUIRE(M >= 1 && C >= 1 && ld >= C && ldy >= C && (!dA || ldd >= C) && (dA || ldo >= C),
+    PN2_REQUIRE(M >= 1 && M < ((int64_t)1 << 31) && C >= 1 && ld >= C && ldy >= C && (!dA || ldd >= C) &&
+                    (dA || ldo >= C),
                 "pn2_bn_relu_backward_f32: bad shape");
     PN2_REQUIRE(ws_bytes >= pn2_bn_train_workspace_bytes(M, C), "pn2_bn_relu_backward_f32: workspace too small");
+    PN2_REQUIRE((flags & ~PN2_LAYER_NO_RELU) == 0, "pn2_bn_relu_backward_f32: unknown flags");
+    const int relu = (flags & PN2_LAYER_NO_RELU) ? 0 : 1;
     hipStream_t st = as_stream(stream);
     double *part = static_cast<double *>(ws);
-    double *sums = part + chunks(M) * 2 * C;
-    hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)chunks(M)),
-                       dim3(256), 0, st, Y, M, C, ld, mean, invstd, gamma, beta, dA, ldd, dOut, ldo, arg, K, part);
+    double *sums = part + chunks(M, C) * 2 * C;
+    hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)chunks(M, C)),
+                       dim3(256), 0, st, Y, M, C, ld, mean, invstd, gamma, beta, dA, ldd, dOut, ldo, arg, K, relu,
+                       chunk_rows(M, C), part);
     PN2_LAUNCH_CHECK("bn_bwd_partial_kernel");
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((unsigned)C), dim3(64), 0, st, part, chunks(M), M, C, gamma,
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((unsigned)C), dim3(64), 0, st, part, chunks(M, C), M, C, gamma,
                        invstd, sxhat, dbeta, dgamma, dbias, sums);
     PN2_LAUNCH_CHECK("bn_bwd_final_kernel");
     hipLaunchKernelGGL(bn_bwd_apply_kernel,
                        dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)((M + kTrEwRows - 1) / kTrEwRows)),
                        dim3(256), 0, st, Y, M, C, ld, mean, invstd, gamma, beta, dA, ldd, dOut, ldo, arg, K,
-                       sums, dY, ldy);
+                       relu, sums, dY, ldy);
     PN2_LAUNCH_CHECK("bn_bwd_apply_kernel");
     return PN2_OK;
 }

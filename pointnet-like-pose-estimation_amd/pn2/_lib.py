@@ -74,11 +74,14 @@ SIGNATURES = {
     "pn2_bn_train_workspace_bytes": (_i64, [_i64, _i64]),
     "pn2_bn_train_stats_f32": (_int, [_vp, _i64, _i64, _i64, ctypes.c_double, ctypes.c_double, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
-    "pn2_bn_relu_apply_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "pn2_bn_relu_apply_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _int,
+                                     _vp]),
+    "pn2_bn_train_forward_f32": (_int, [_vp, _i64, _i64, _i64, ctypes.c_double, ctypes.c_double, _vp,
+                                        _vp, _vp, _vp, _vp, _i64, _int, _vp, _vp, _vp, _i64, _vp]),
     "pn2_group_max_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp]),
     "pn2_bn_relu_backward_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
                                         _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64,
-                                        _vp]),
+                                        _int, _vp]),
     "pn2_prepare_points_f64": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _vp, _i64,
                                       _vp, _vp, _vp]),
     "pn2_pack_layer_split_bf16": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp]),
@@ -90,7 +93,7 @@ SIGNATURES = {
                                    _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 _lib = None
 
 

@@ -5,8 +5,9 @@ Like heads.py: submodules are created in the reference's order, so ``torch.manua
 before construction gives the identical parameters (pinned by the state_dict hash in the
 v1_*.npz goldens) and the ``state_dict`` keys match the reference's checkpoints.  The per-point
 shared MLP + max over the points -- the whole cost of these networks -- runs on the split-bf16
-dense-layer kernels through ``point_mlp`` in eval mode on the GPU; the FC tails are [B, 1024]
-library GEMMs (torch).
+dense-layer kernels through ``point_mlp`` in eval mode on the GPU, and on pn2.train's fused
+batch-statistics kernels when training on the GPU; the FC tails are [B, 1024] library GEMMs
+(torch).
 
   PointNetCls    /root/reference/model/pointnet_cls.py:7-32
   RotationV1     /root/reference/model/rotation.py:7-50 (its T-Net output is computed and
@@ -20,8 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .pointnet2_utils import _needs_autograd
-from .pointnet_utils import PointNetEncoder, TNet3d, TNetkd, _rows_to_cf, point_mlp
+from .pointnet_utils import PointNetEncoder, TNet3d, TNetkd, _rows_to_cf, mlp_mode, run_mlp
 
 
 class _ConvStack(nn.Module):
@@ -44,22 +44,23 @@ class _ConvStack(nn.Module):
             cin = cout
         self._caches = {}
 
-    def _fused(self, x):
-        """Eval without autograd: the HIP kernels (device tensors only -- a CPU tensor raises,
-        there is no CPU fallback).  Otherwise the reference's torch formulation."""
-        return not _needs_autograd(self, x)
+    def _mode(self, x):
+        """mlp_mode over the whole conv stack: "fused" (eval without autograd: the HIP kernels,
+        device tensors only -- a CPU tensor raises, there is no CPU fallback), "train" (training
+        on the device: pn2.train) or "torch" (the reference's formulation)."""
+        return mlp_mode(self, x, list(self.conv), list(self.bn_conv))
 
-    def _layers(self, x, lo, hi, pool):
+    def _layers(self, x, lo, hi, pool, mode, rows=False):
         """relu(bn_conv[i](conv[i](x))) for i in [lo, hi), then the max over the points when
-        pool.  Eval on the GPU: x channel-first [B, C<=16, N] or rows [B, N, C]; returns
-        [B, 1024] (pool) or rows [B, N, cout].  Otherwise the reference's torch ops on
-        channel-first tensors."""
-        if not self._fused(x):
+        pool.  "fused" / "train": x channel-first [B, C, N] as the head received it, or rows
+        [B, N, C] (rows=True) from a previous call; returns [B, 1024] (pool) or rows
+        [B, N, cout].  "torch": the reference's ops on channel-first tensors."""
+        if mode == "torch":
             for i in range(lo, hi):
                 x = F.relu(self.bn_conv[i](self.conv[i](x)))
             return torch.max(x, 2, keepdim=True)[0].view(-1, x.shape[1]) if pool else x
-        return point_mlp(x, list(self.conv[lo:hi]), list(self.bn_conv[lo:hi]),
-                         self._caches.setdefault((lo, hi), {}), pool=pool, module=self)
+        return run_mlp(mode, x, list(self.conv[lo:hi]), list(self.bn_conv[lo:hi]),
+                       self._caches.setdefault((lo, hi), {}), pool=pool, module=self, rows=rows)
 
     def _tail(self, x):
         """fc / bn_fc / dropout / relu for all but the last fc (rotation.py:45-49)."""
@@ -70,11 +71,12 @@ class _ConvStack(nn.Module):
                 x = self.fc[i](x)
         return x
 
-    def _split_ftnet(self, x):
+    def _split_ftnet(self, x, mode):
         """Layers 0-1, the feature T-Net on their output, layers 2.. + max (rotation.py:37-43,
-        pose.py:59-69).  Returns (layer-1 output -- rows on the fused path, else channel-first -- and the T-Net's T)."""
-        h = self._layers(x, 0, 2, pool=False)
-        if self._fused(x):
+        pose.py:59-69).  Returns (layer-1 output -- rows unless mode is "torch", then
+        channel-first -- and the T-Net's T)."""
+        h = self._layers(x, 0, 2, False, mode)
+        if mode != "torch":
             return h, self.ftnet(_rows_to_cf(h))
         return h, self.ftnet(h)
 
@@ -106,8 +108,9 @@ class RotationV1(_ConvStack):
         self.dropout = nn.Dropout(p=0.4)
 
     def forward(self, x):
-        h, _ = self._split_ftnet(x)
-        return self._tail(self._layers(h, 2, len(self.conv), pool=True))
+        mode = self._mode(x)
+        h, _ = self._split_ftnet(x, mode)
+        return self._tail(self._layers(h, 2, len(self.conv), True, mode, rows=mode != "torch"))
 
 
 class TranslationV1(_ConvStack):
@@ -125,7 +128,7 @@ class TranslationV1(_ConvStack):
     def forward(self, x, mean):
         if self.mean_mlp == 'True':
             mean = self.fc2(F.relu(self.bn1(self.fc1(mean))))
-        return self._tail(self._layers(x, 0, len(self.conv), pool=True)) + mean
+        return self._tail(self._layers(x, 0, len(self.conv), True, self._mode(x))) + mean
 
 
 class SignV1(_ConvStack):
@@ -135,7 +138,7 @@ class SignV1(_ConvStack):
         self.dropout = nn.Dropout(p=0.4)
 
     def forward(self, x):
-        x = torch.sigmoid(self._tail(self._layers(x, 0, len(self.conv), pool=True)))
+        x = torch.sigmoid(self._tail(self._layers(x, 0, len(self.conv), True, self._mode(x))))
         return x, torch.sign(x - 0.5)
 
 
@@ -147,7 +150,7 @@ class WidthV1(_ConvStack):
         self.dropout = nn.Dropout(p=0.4)
 
     def forward(self, x):
-        return self._tail(self._layers(x, 0, len(self.conv), pool=True))
+        return self._tail(self._layers(x, 0, len(self.conv), True, self._mode(x)))
 
 
 class PoseV1(_ConvStack):
@@ -183,15 +186,16 @@ class PoseV1(_ConvStack):
             x = torch.bmm(transform, x)
             if D > 3:
                 x = torch.cat([x, normal], dim=2)  # the reference's axis (pose.py:57)
+        mode = self._mode(x)
         if self.feat_trans:
-            h, trans_feat = self._split_ftnet(x)
-            if self._fused(x):  # bmm(trans_feat, x) in the rows layout
+            h, trans_feat = self._split_ftnet(x, mode)
+            if mode != "torch":  # bmm(trans_feat, x) in the rows layout
                 h = torch.bmm(h, trans_feat.transpose(1, 2))
             else:
                 h = torch.bmm(trans_feat, h)
-            x = self._layers(h, 2, len(self.conv), pool=True)
+            x = self._layers(h, 2, len(self.conv), True, mode, rows=mode != "torch")
         else:
-            x = self._layers(x, 0, len(self.conv), pool=True)
+            x = self._layers(x, 0, len(self.conv), True, mode)
         x = self._tail(x)
         if self.mean:
             mean = torch.mean(x[:, :3, :], dim=2)

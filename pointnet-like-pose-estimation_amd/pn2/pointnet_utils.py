@@ -18,8 +18,10 @@ with a group_all source for a channel-first [B,C<=16,N] input, or a rows source 
 features already in HBM), one launch per layer, the max fused into the last layer's epilogue;
 the encoder's conv3 + bn3 without ReLU before its max uses PN2_LAYER_NO_RELU (signed pooling).
 The small per-cloud transforms (torch.bmm of a 3x3 / 64x64 matrix with the points) and the
-T-Nets' FC layers are plain library GEMMs (torch on the GPU).  Training / autograd keeps the
-reference's torch formulation.
+T-Nets' FC layers are plain library GEMMs (torch on the GPU).  Training on the GPU runs the same
+shared MLPs through pn2.train.point_mlp_train (library GEMMs + the fused batch-statistics BN /
+ReLU / max kernels, forward and backward) in the same rows layout; eval with autograd (and
+exotic BN configurations) keeps the reference's torch formulation.
 """
 import numpy as np
 import torch
@@ -28,6 +30,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import ops
+from . import train
 from .pointnet2_utils import _needs_autograd, _precision
 
 
@@ -56,12 +59,15 @@ def _pack(convs, bns, cache, xyz):
     return cache["layers"]
 
 
-def point_mlp(x, convs, bns, cache, pool=True, last_relu=True, module=None):
+def point_mlp(x, convs, bns, cache, pool=True, last_relu=True, module=None, rows=False):
     """relu(bn(conv(x))) over every point (the last layer without ReLU if not last_relu), then
-    the max over the points when pool.  x: channel-first [B, C, N] (C <= 16, read in place) or
-    per-point rows [B, N, C] (unit column stride, as a previous point_mlp returns them).
+    the max over the points when pool.  x: channel-first [B, C, N] (rows=False, any strides:
+    C <= 16 is read in place as a group_all source, wider inputs as rows) or per-point rows
+    [B, N, C] (rows=True, unit column stride, as a previous point_mlp returns them).
     Returns [B, cout] (pool) or rows [B, N, cout]."""
-    chan_first = x.shape[1] <= 16 and x.stride(1) != 1
+    if not rows and x.shape[1] > 16:
+        x, rows = _cf_to_rows(x), True
+    chan_first = not rows
     if chan_first:
         B, C, N = x.shape
         pts = x.permute(0, 2, 1)
@@ -80,9 +86,9 @@ def point_mlp(x, convs, bns, cache, pool=True, last_relu=True, module=None):
     # the kernels take <= 4 layers per call: longer chains go through a rows intermediate
     if n > 4:
         mid = point_mlp(x, convs[:n - 3], bns[:n - 3], cache.setdefault("head", {}), pool=False,
-                        module=module)
+                        module=module, rows=rows)
         return point_mlp(mid, convs[n - 3:], bns[n - 3:], cache.setdefault("tail", {}), pool,
-                         last_relu, module)
+                         last_relu, module, rows=True)
     if chan_first:
         ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_ALL, pts, None, None, None, wts, als, bes, cins,
                               splits, prec, flags, pool=pool)
@@ -90,6 +96,27 @@ def point_mlp(x, convs, bns, cache, pool=True, last_relu=True, module=None):
         ops.sa_mlp_max_direct(out, _lib.SRC_ROWS, None, None, None, None, wts, als, bes, cins,
                               splits, prec, flags, rows=x, pool=pool)
     return out if pool else out.view(B, N, cout)
+
+
+def mlp_mode(module, x, convs, bns):
+    """How a v1 module runs its shared MLPs on x: "fused" (eval without autograd: the split-bf16
+    kernels; a CPU tensor raises), "train" (training on the device: pn2.train), or "torch" (the
+    reference's formulation: eval with autograd, CPU training, BN configs pn2.train does not
+    cover)."""
+    if not _needs_autograd(module, x):
+        return "fused"
+    if module.training and train.eligible(x, convs, bns):
+        return "train"
+    return "torch"
+
+
+def run_mlp(mode, x, convs, bns, cache, pool=True, last_relu=True, module=None, rows=False):
+    """point_mlp ("fused") or train.point_mlp_train ("train") on x: channel-first [B, C, N]
+    as the module received it (rows=False), or rows [B, N, C] from a previous run_mlp
+    (rows=True).  Same results layout: [B, cout] (pool) or rows [B, N, cout]."""
+    if mode == "train":
+        return train.point_mlp_train(x, convs, bns, rows, pool, last_relu)
+    return point_mlp(x, convs, bns, cache, pool, last_relu, module, rows)
 
 
 def _rows_to_cf(rows):
@@ -132,15 +159,15 @@ class _TNet(nn.Module):
     def forward(self, x):
         """x: [B, C, N] (any strides: a rows view is read as rows, not copied)."""
         B = x.size()[0]
-        if _needs_autograd(self, x):
+        convs, bns = [self.conv1, self.conv2, self.conv3], [self.bn1, self.bn2, self.bn3]
+        mode = mlp_mode(self, x, convs, bns)
+        if mode == "torch":
             h = F.relu(self.bn1(self.conv1(x)))
             h = F.relu(self.bn2(self.conv2(h)))
             h = F.relu(self.bn3(self.conv3(h)))
             g = torch.max(h, 2, keepdim=True)[0].view(-1, 1024)
         else:
-            g = point_mlp(x if x.shape[1] <= 16 and x.stride(1) != 1 else _cf_to_rows(x),
-                          [self.conv1, self.conv2, self.conv3], [self.bn1, self.bn2, self.bn3],
-                          self._cache, module=self)
+            g = run_mlp(mode, x, convs, bns, self._cache, module=self)
         g = F.relu(self.bn4(self.fc1(g)))
         g = F.relu(self.bn5(self.fc2(g)))
         g = self.fc3(g)
@@ -186,7 +213,8 @@ class PointNetEncoder(nn.Module):
         x = torch.bmm(transform, x)
         if D > 3:
             x = torch.cat([x, normal], dim=2)  # the reference's concatenation axis (:112)
-        if _needs_autograd(self, x):
+        mode = mlp_mode(self, x, [self.conv1, self.conv2, self.conv3], [self.bn1, self.bn2, self.bn3])
+        if mode == "torch":
             x = F.relu(self.bn1(self.conv1(x)))
             trans_feat = self.ftnet(x)
             x = torch.bmm(trans_feat, x)
@@ -196,14 +224,14 @@ class PointNetEncoder(nn.Module):
             x = torch.max(x, 2, keepdim=True)[0].view(-1, 1024)
         else:
             # conv1 + bn1 + relu per point -> rows [B, N, 64]
-            r1 = point_mlp(x, [self.conv1], [self.bn1], self._c1, pool=False, module=self)
+            r1 = run_mlp(mode, x, [self.conv1], [self.bn1], self._c1, pool=False, module=self)
             trans_feat = self.ftnet(_rows_to_cf(r1))
             # bmm(trans_feat, x) in the rows layout: x2 rows = x1 rows . trans_feat^T
             r2 = torch.bmm(r1, trans_feat.transpose(1, 2))
             pointfeat = _rows_to_cf(r2)
             # conv2 + bn2 + relu, conv3 + bn3 (no ReLU, :126-127), max over the points
-            x = point_mlp(r2, [self.conv2, self.conv3], [self.bn2, self.bn3], self._c23,
-                          last_relu=False, module=self)
+            x = run_mlp(mode, r2, [self.conv2, self.conv3], [self.bn2, self.bn3], self._c23,
+                        last_relu=False, module=self, rows=True)
         if self.global_feat:
             return x, transform, trans_feat
         x = x.view(-1, 1024, 1).repeat(1, 1, N)
@@ -217,4 +245,5 @@ def feature_transform_reguliarzer(transform):
     return torch.mean(torch.norm(torch.bmm(transform, transform.transpose(2, 1)) - I, dim=(1, 2)))
 
 
-__all__ = ["TNet3d", "TNetkd", "PointNetEncoder", "feature_transform_reguliarzer", "point_mlp"]
+__all__ = ["TNet3d", "TNetkd", "PointNetEncoder", "feature_transform_reguliarzer", "point_mlp",
+           "mlp_mode", "run_mlp"]

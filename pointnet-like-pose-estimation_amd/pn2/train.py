@@ -12,8 +12,15 @@ max + argmax and their backward are the fused HIP kernels of csrc/train.hip (one
 activations each).  BatchNorm semantics follow torch's train mode: biased variance normalises,
 running_var takes the unbiased one, momentum None = cumulative average, num_batches_tracked += 1.
 
-Used by the SA modules' autograd path when a module is training on a ROCm device (pn2/
-pointnet2_utils.py); eval with autograd keeps the reference's torch formulation.
+The PointNet-v1 shared MLPs (Conv1d 1x1 -> train-mode BatchNorm1d -> ReLU, /root/reference/
+model/pointnet_utils.py:31-35, 118-128, and the v1 heads' conv stacks, rotation.py:37-43) are the
+same computation on [M = B*N, C] rows with K = N (the max over a cloud's points) or no max at all
+(the encoder's per-point conv1); the encoder's conv3 + bn3 before its max has no ReLU
+(PN2_LAYER_NO_RELU): point_mlp_train.
+
+Used by the SA modules' and the v1 modules' autograd path when a module is training on a ROCm
+device (pn2/pointnet2_utils.py, pn2/pointnet_utils.py, pn2/heads_v1.py); eval with autograd
+keeps the reference's torch formulation.
 """
 import torch
 
@@ -23,11 +30,12 @@ from .ops import _stream
 
 
 def eligible(grouped, convs, bns):
-    """The fused training path covers: device rows, 1x1 convs with bias, affine train-mode BN."""
+    """The fused training path covers: device rows, 1x1 convs (Conv2d or Conv1d) with bias,
+    affine train-mode BN."""
     if not grouped.is_cuda or grouped.dtype != torch.float32:
         return False
     for conv, bn in zip(convs, bns):
-        if conv.bias is None or tuple(conv.weight.shape[2:]) != (1, 1) or not bn.affine:
+        if conv.bias is None or tuple(conv.weight.shape[2:]) not in ((1, 1), (1,)) or not bn.affine:
             return False
         if not bn.training:
             return False
@@ -64,51 +72,65 @@ def _grad_weight(dY, X):
     return g
 
 
+_WS = {}
+
+
+def _workspace(L, M, C, device, stream):
+    """The BN sweeps' float64 partials, one grow-only buffer per (device, stream): every use is
+    ordered on that stream, so forward and backward layers can share it (one allocation per
+    step instead of one per call)."""
+    need = int(L.pn2_bn_train_workspace_bytes(M, C))
+    key = (device, stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(max(need, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = ws
+    return ws
+
+
 class _MlpMaxTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x0, K, cfg, *params):
-        """x0 [M, Cin] rows; cfg[l] = (eps, momentum factor, running_mean, running_var);
-        params = (W, b, gamma, beta) per layer.  -> [M / K, Cout] max over each K rows."""
+        """x0 [M, Cin] rows; cfg[l] = (eps, momentum factor, running_mean, running_var, flags);
+        params = (W, b, gamma, beta) per layer.  -> [M / K, Cout] max over each K rows, or the
+        last layer's [M, Cout] rows when K == 0."""
         L = _lib.load()
         n = len(cfg)
         M = x0.shape[0]
         st = _stream(x0)
         xs, ys, stats = [x0], [], []
         x = x0
-        ws = None
         for l in range(n):
             W, b, g, be = params[4 * l:4 * l + 4]
-            eps, mom, rm, rv = cfg[l]
+            eps, mom, rm, rv, flags = cfg[l]
             cout = W.shape[0]
             Y = torch.addmm(b, x, W.reshape(cout, -1).t())
-            wsb = int(L.pn2_bn_train_workspace_bytes(M, cout))
-            if ws is None or ws.numel() < wsb:
-                ws = torch.empty(wsb, dtype=torch.uint8, device=x0.device)
-            mean = torch.empty(cout, device=x0.device)
-            invstd = torch.empty(cout, device=x0.device)
+            ws = _workspace(L, M, cout, x0.device, st)
+            st_mi = torch.empty(2 * cout, device=x0.device)  # [mean | invstd]
             sxhat = torch.empty(cout, dtype=torch.float64, device=x0.device)
             upd = mom > 0.0 and rm is not None
-            _lib.check(L.pn2_bn_train_stats_f32(
-                Y.data_ptr(), M, cout, cout, float(eps), float(mom) if upd else 0.0,
-                rm.data_ptr() if upd else 0, rv.data_ptr() if upd else 0, mean.data_ptr(),
-                invstd.data_ptr(), sxhat.data_ptr(), ws.data_ptr(), ws.numel(), st),
-                "pn2_bn_train_stats_f32")
             A = torch.empty_like(Y)
-            _lib.check(L.pn2_bn_relu_apply_f32(Y.data_ptr(), M, cout, cout, mean.data_ptr(),
-                                               invstd.data_ptr(), g.data_ptr(), be.data_ptr(),
-                                               A.data_ptr(), cout, st), "pn2_bn_relu_apply_f32")
+            _lib.check(L.pn2_bn_train_forward_f32(
+                Y.data_ptr(), M, cout, cout, float(eps), float(mom) if upd else 0.0,
+                rm.data_ptr() if upd else 0, rv.data_ptr() if upd else 0, g.data_ptr(),
+                be.data_ptr(), A.data_ptr(), cout, flags, st_mi.data_ptr(), sxhat.data_ptr(),
+                ws.data_ptr(), ws.numel(), st), "pn2_bn_train_forward_f32")
             ys.append(Y)
-            stats += [mean, invstd, sxhat]
+            stats += [st_mi[:cout], st_mi[cout:], sxhat]
             x = A
             if l + 1 < n:
                 xs.append(A)
+        ctx.K, ctx.n = K, n
+        ctx.flags = tuple(c[4] for c in cfg)
+        if not K:
+            ctx.save_for_backward(*xs, *ys, *stats, *params)
+            return x
         G = M // K
         cout = x.shape[1]
         out = torch.empty(G, cout, device=x0.device)
         arg = torch.empty(G, cout, dtype=torch.int32, device=x0.device)
         _lib.check(L.pn2_group_max_f32(x.data_ptr(), G, K, cout, cout, out.data_ptr(), cout,
                                        arg.data_ptr(), st), "pn2_group_max_f32")
-        ctx.K, ctx.n = K, n
         ctx.save_for_backward(*xs, *ys, *stats, arg, *params)
         return out
 
@@ -120,33 +142,31 @@ class _MlpMaxTrain(torch.autograd.Function):
         xs = saved[:n]
         ys = saved[n:2 * n]
         stats = saved[2 * n:5 * n]
-        arg = saved[5 * n]
-        params = saved[5 * n + 1:]
+        arg = saved[5 * n] if K else None
+        params = saved[5 * n + (1 if K else 0):]
         dout = dout.contiguous()
         M = xs[0].shape[0]
         st = _stream(dout)
         grads = [None] * (4 * n)
-        dA = None
-        ws = None
+        dA = None if K else dout  # K == 0: the rows' gradient is dense
         for l in reversed(range(n)):
             W, b, g, be = params[4 * l:4 * l + 4]
             Y = ys[l]
             mean, invstd, sxhat = stats[3 * l], stats[3 * l + 1], stats[3 * l + 2]
             cout = Y.shape[1]
-            wsb = int(L.pn2_bn_train_workspace_bytes(M, cout))
-            if ws is None or ws.numel() < wsb:
-                ws = torch.empty(wsb, dtype=torch.uint8, device=Y.device)
+            ws = _workspace(L, M, cout, Y.device, st)
             dY = torch.empty_like(Y)
             dgamma = torch.empty(cout, device=Y.device)
             dbeta = torch.empty(cout, device=Y.device)
             dbias = torch.empty(cout, device=Y.device)
-            last = dA is None
+            last = l == n - 1 and K
             _lib.check(L.pn2_bn_relu_backward_f32(
                 Y.data_ptr(), M, cout, cout, mean.data_ptr(), invstd.data_ptr(), g.data_ptr(),
                 be.data_ptr(), 0 if last else dA.data_ptr(), cout,
                 dout.data_ptr() if last else 0, cout, arg.data_ptr() if last else 0, K,
                 sxhat.data_ptr(), dY.data_ptr(), cout, dgamma.data_ptr(), dbeta.data_ptr(),
-                dbias.data_ptr(), ws.data_ptr(), ws.numel(), st), "pn2_bn_relu_backward_f32")
+                dbias.data_ptr(), ws.data_ptr(), ws.numel(), ctx.flags[l], st),
+                "pn2_bn_relu_backward_f32")
             X = xs[l]
             W2 = W.reshape(cout, -1)
             grads[4 * l] = _grad_weight(dY, X).view_as(W)
@@ -192,6 +212,18 @@ def group_train(points, idx, centers, feature, feature_first):
     return _GroupTrain.apply(feature, points, centers, idx, feature_first)
 
 
+def _apply(x0, K, convs, bns, last_relu=True):
+    cfg, params = [], []
+    n = len(convs)
+    for l, (conv, bn) in enumerate(zip(convs, bns)):
+        mom = _bn_factor(bn)
+        flags = _lib.LAYER_NO_RELU if (l == n - 1 and not last_relu) else 0
+        cfg.append((bn.eps, mom, bn.running_mean if mom > 0 else None,
+                    bn.running_var if mom > 0 else None, flags))
+        params += [conv.weight, conv.bias, bn.weight, bn.bias]
+    return _MlpMaxTrain.apply(x0, K, tuple(cfg), *params)
+
+
 def mlp_max_train(grouped, convs, bns):
     """grouped [B, S, K, Cin] (any float32 device tensor, autograd-tracked) -> [B, Cout, S]:
     the reference's ``torch.max(relu(bn(conv(x)))..., 2)[0]`` in train mode (:167-172)."""
@@ -199,14 +231,26 @@ def mlp_max_train(grouped, convs, bns):
     x0 = grouped.reshape(B * S * K, Cin)
     if not x0.is_contiguous():
         x0 = x0.contiguous()
-    cfg, params = [], []
-    for conv, bn in zip(convs, bns):
-        mom = _bn_factor(bn)
-        cfg.append((bn.eps, mom, bn.running_mean if mom > 0 else None,
-                    bn.running_var if mom > 0 else None))
-        params += [conv.weight, conv.bias, bn.weight, bn.bias]
-    out = _MlpMaxTrain.apply(x0, K, tuple(cfg), *params)
+    out = _apply(x0, K, convs, bns)
     return out.view(B, S, -1).permute(0, 2, 1)
 
 
-__all__ = ["mlp_max_train", "group_train", "eligible"]
+def point_mlp_train(x, convs, bns, rows, pool=True, last_relu=True):
+    """The v1 shared MLP in train mode, pn2.pointnet_utils.point_mlp's contract: x channel-first
+    [B, C, N] (rows=False) or per-point rows [B, N, C] (rows=True), autograd-tracked; returns
+    the max over the points [B, Cout] (pool) or rows [B, N, Cout].  The reference's
+    relu(bn(conv(x)))* (+ torch.max(x, 2)) with Conv1d / BatchNorm1d in train mode
+    (pointnet_utils.py:31-35, 118-128); last_relu=False drops the last ReLU (:127)."""
+    if rows:
+        B, N, C = x.shape
+        x0 = x.reshape(B * N, C)
+    else:
+        B, C, N = x.shape
+        x0 = x.permute(0, 2, 1).reshape(B * N, C)
+    if not x0.is_contiguous():
+        x0 = x0.contiguous()
+    out = _apply(x0, N if pool else 0, convs, bns, last_relu)
+    return out if pool else out.view(B, N, -1)
+
+
+__all__ = ["mlp_max_train", "point_mlp_train", "group_train", "eligible"]

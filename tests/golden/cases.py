@@ -154,6 +154,43 @@ TRAIN_CASES = {
 }
 
 
+# PointNet-v1 training cases: name -> (head module, B, N, cloud kind, weight seed, get_model
+# kwargs).  Train mode with every Dropout switched to eval (its mask is device-RNG dependent);
+# loss = sum_i (out_i * R_i) over the head's float outputs.  Seeds are chosen so that every max
+# over the points is tie-free: the smallest relative gap between a (cloud, channel)'s two largest
+# values is >= TRAIN_V1_MIN_GAP in the float64 forward (a pair closer than float32 noise may
+# route that channel's gradient to another point in any fp32 implementation, the reference's
+# own included); make_goldens.py records and checks it.
+TRAIN_V1_CASES = {
+    'cls': ('pointnet_cls', 4, 96, 'uniform3', 3010, {}),
+    'rotation': ('rotation', 4, 96, 'onehot10', 1011, {}),
+    'pose': ('pose', 4, 96, 'uniform3', 1286,
+             {'mlp_list': [64, 64, 64, 128, 1024], 'linear_list': [512, 256, 2],
+              'classify': True, 'num_category': 0, 'normal_channel': False,
+              'transform': True, 'feat_trans': True}),
+}
+TRAIN_V1_MIN_GAP = 2e-5
+
+
+def train_v1_model(factory, wseed, **kw):
+    """build_head, then train mode with the dropouts off."""
+    model = build_head(factory, wseed, **kw).train()
+    for m in model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.eval()
+    return model
+
+
+GRAD_FULL_MAX = 32768   # larger gradients are kept as a fixed sample + their norm
+GRAD_SAMPLE = 8192
+
+
+def grad_sample_index(n):
+    """The flat indices of an n-element gradient kept in the trainv1 goldens (sorted, fixed by
+    n alone)."""
+    return np.sort(np.random.default_rng(n).choice(n, GRAD_SAMPLE, replace=False))
+
+
 def train_inputs(B, N, D, seed):
     """points [B, 3, N] (unit-sphere cloud, channel-first), feature [B, D, N] or None, and the
     loss weights R are drawn by the caller once the output shape is known."""

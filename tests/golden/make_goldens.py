@@ -209,6 +209,79 @@ def gen_train(P):
         print("train", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
 
 
+def _v1_step_record(model, x, Rs, prefix, rec):
+    """One train step of a v1 head (loss = sum_i out_i * R_i; R drawn here when Rs is empty):
+    outputs, parameter gradients (large ones as a fixed sample + norm) under `prefix`."""
+    out = model(x)
+    outs = [o for o in (out if isinstance(out, tuple) else (out,))
+            if torch.is_tensor(o) and o.is_floating_point() and o.requires_grad]
+    loss = 0
+    for i, o in enumerate(outs):
+        if len(Rs) <= i:
+            Rs.append(torch.randn(o.shape, generator=torch.Generator().manual_seed(len(Rs) + 77)))
+        loss = loss + (o * Rs[i].to(o.dtype)).sum()
+        rec[prefix + "out%d" % i] = o.detach().float().numpy()
+    loss.backward()
+    for k, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        gr = p.grad.float().numpy()
+        if gr.size > cases.GRAD_FULL_MAX:  # the FC / conv3 weights: a fixed sample + norm
+            rec[prefix + "gsub." + k] = gr.reshape(-1)[cases.grad_sample_index(gr.size)]
+            rec[prefix + "gnorm." + k] = np.array(np.linalg.norm(p.grad.double().numpy()))
+        else:
+            rec[prefix + "grad." + k] = gr
+    return len(outs)
+
+
+def _v1_min_gap(model):
+    """Forward hooks on the BatchNorm before each max over the points: the smallest relative
+    gap between a (cloud, channel)'s two largest (ReLU'd, except the encoder's conv3) values."""
+    gaps = []
+    last = "bn_conv.%d" % (len(getattr(model, "conv", [])) - 1)
+    for k, m in model.named_modules():
+        if not (k.endswith("bn3") or k == last):
+            continue
+        signed = k.endswith("feat.bn3") or k == "bn3"
+
+        def f(_m, _i, out, signed=signed):
+            h = out.detach() if signed else torch.relu(out.detach())
+            t2 = torch.topk(h, 2, dim=2)[0]
+            rel = (t2[..., 0] - t2[..., 1]) / t2[..., 0].abs().clamp_min(1e-300)
+            rel = rel.flatten() if signed else rel[t2[..., 0] > 0]
+            if rel.numel():
+                gaps.append(float(rel.min()))
+        m.register_forward_hook(f)
+    return gaps
+
+
+def gen_train_v1(importlib):
+    """Training-mode forward + backward of the PointNet-v1 heads with the reference modules
+    (pointnet_utils.py T-Nets / encoder and the heads' conv stacks): outputs, every parameter
+    gradient and the running statistics after the step, in float32 (the reference as it runs)
+    and the same step in float64 ("t." keys: the precision reference the GPU test measures
+    against -- these deep T-Net networks amplify float32 rounding to ~1e-3 in some gradients,
+    the reference's own float32 step included)."""
+    for name, (head, B, N, kind, wseed, kw) in cases.TRAIN_V1_CASES.items():
+        mod = importlib.import_module(head)
+        model = cases.train_v1_model(mod.get_model, wseed, **kw)
+        x = cases.cloud(kind, B, N, wseed + 7).permute(0, 2, 1).contiguous()
+        rec = {"input": x.numpy(), "state_hash": np.array(cases.state_hash(model))}
+        Rs = []
+        n = _v1_step_record(model, x, Rs, "", rec)
+        for i, R in enumerate(Rs):
+            rec["R%d" % i] = R.numpy()
+        for k, b in model.named_buffers():
+            rec["buf." + k] = b.numpy()
+        m64 = cases.train_v1_model(mod.get_model, wseed, **kw).double()
+        gaps = _v1_min_gap(m64)
+        _v1_step_record(m64, x.double(), Rs, "t.", rec)
+        rec["min_gap"] = np.array(min(gaps))
+        assert min(gaps) >= cases.TRAIN_V1_MIN_GAP, (name, gaps)
+        np.savez_compressed(os.path.join(HERE, "trainv1_%s.npz" % name), **rec)
+        print("trainv1", name, n, "outputs, min gap %.1e" % min(gaps))
+
+
 def main():
     torch.set_num_threads(8)
     P, importlib = _ref()
@@ -223,6 +296,8 @@ def main():
         gen_prep()
     if not only or "train" in only:
         gen_train(P)
+    if not only or "trainv1" in only:
+        gen_train_v1(importlib)
     meta = {
         "torch": torch.__version__,
         "cpu_capability": torch.backends.cpu.get_cpu_capability(),

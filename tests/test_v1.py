@@ -174,24 +174,33 @@ def _rand_layers(cins, couts, seed):
     (2, 500, 128, [1024], True, False),
     (4, 300, 64, [64], False, True),            # unpooled rows out
     (1, 33, 64, [128, 256], False, False),      # unpooled, signed
+    (2, 8, 64, [64, 128], True, True),          # fewer points than 16 (rows, not channels)
 ])
 def test_point_mlp_rows_source(B, N, cin, couts, pool, relu_last):
     from pn2.pointnet_utils import point_mlp
     convs, bns = _rand_layers([cin] + couts[:-1], couts, 11 + N)
     rows = torch.randn(B, N, cin, device="cuda")
     with torch.no_grad():
-        got = point_mlp(rows, convs, bns, {}, pool=pool, last_relu=relu_last)
+        got = point_mlp(rows, convs, bns, {}, pool=pool, last_relu=relu_last, rows=True)
         ref = _torch_layers(rows.permute(0, 2, 1), convs, bns, relu_last)
         ref = ref.max(2)[0] if pool else ref.permute(0, 2, 1)
     assert_close(got.cpu().numpy(), ref.cpu().numpy(), 1e-5)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("C,N,pool", [(3, 1024, False), (10, 2048, True), (13, 100, True), (3, 5, False)])
-def test_point_mlp_channel_first_source(C, N, pool):
+@pytest.mark.parametrize("C,N,pool,tview", [(3, 1024, False, False), (10, 2048, True, False),
+                                            (13, 100, True, False), (3, 5, False, False),
+                                            (10, 1024, True, True), (3, 7, False, True),
+                                            (64, 300, True, True)])
+def test_point_mlp_channel_first_source(C, N, pool, tview):
+    """tview: the input is the transpose(2, 1) view of [B, N, C] storage -- the layout the
+    reference's scripts (and pn2.provider.prepare_batch) hand the model."""
     from pn2.pointnet_utils import point_mlp
     convs, bns = _rand_layers([C], [64], 7 + C)
-    x = torch.randn(2, C, N, device="cuda")
+    if tview:
+        x = torch.randn(2, N, C, device="cuda").transpose(2, 1)
+    else:
+        x = torch.randn(2, C, N, device="cuda")
     with torch.no_grad():
         got = point_mlp(x, convs, bns, {}, pool=pool)
         ref = _torch_layers(x, convs, bns)
