@@ -7,7 +7,7 @@ v1_*.npz goldens) and the ``state_dict`` keys match the reference's checkpoints.
 shared MLP + max over the points -- the whole cost of these networks -- runs on the split-bf16
 dense-layer kernels through ``point_mlp`` in eval mode on the GPU, and on pn2.train's fused
 batch-statistics kernels when training on the GPU; the FC tails are [B, 1024] library GEMMs
-(torch).
+(torch), each Linear + eval BatchNorm1d folded into one GEMM in eval (``linear_bn``).
 
   PointNetCls    /root/reference/model/pointnet_cls.py:7-32
   RotationV1     /root/reference/model/rotation.py:7-50 (its T-Net output is computed and
@@ -21,7 +21,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .pointnet_utils import PointNetEncoder, TNet3d, TNetkd, _rows_to_cf, mlp_mode, run_mlp
+from .pointnet2_utils import _needs_autograd
+from .pointnet_utils import (PointNetEncoder, TNet3d, TNetkd, _rows_to_cf, linear_bn, mlp_mode,
+                             run_mlp)
 
 
 class _ConvStack(nn.Module):
@@ -43,6 +45,7 @@ class _ConvStack(nn.Module):
             self.bn_fc.append(nn.BatchNorm1d(cout))
             cin = cout
         self._caches = {}
+        self._fc_cache = {}
 
     def _mode(self, x):
         """mlp_mode over the whole conv stack: "fused" (eval without autograd: the HIP kernels,
@@ -62,8 +65,15 @@ class _ConvStack(nn.Module):
         return run_mlp(mode, x, list(self.conv[lo:hi]), list(self.bn_conv[lo:hi]),
                        self._caches.setdefault((lo, hi), {}), pool=pool, module=self, rows=rows)
 
-    def _tail(self, x):
-        """fc / bn_fc / dropout / relu for all but the last fc (rotation.py:45-49)."""
+    def _tail(self, x, mode=None):
+        """fc / bn_fc / dropout / relu for all but the last fc (rotation.py:45-49); "fused":
+        each fc + bn_fc folded into one GEMM (dropout is the identity in eval)."""
+        if mode == "fused":
+            n = len(self.fc)
+            for i in range(n):
+                x = linear_bn(x, self.fc[i], self.bn_fc[i] if i < n - 1 else None,
+                              self._fc_cache.setdefault(i, {}), relu=i < n - 1)
+            return x
         for i in range(len(self.fc)):
             if i < len(self.fc) - 1:
                 x = F.relu(self.dropout(self.bn_fc[i](self.fc[i](x))))
@@ -91,11 +101,16 @@ class PointNetCls(nn.Module):
         self.dropout = nn.Dropout(p=0.4)
         self.bn1 = nn.BatchNorm1d(512)
         self.bn2 = nn.BatchNorm1d(256)
+        self._fc_cache = {}
 
     def forward(self, x):
         x, _, trans_feat = self.feat(x)
-        x = F.relu(self.bn1(self.fc1(x)))
-        x = F.relu(self.bn2(self.dropout(self.fc2(x))))
+        if not _needs_autograd(self, x):  # eval: fc + bn folded (dropout is the identity)
+            x = linear_bn(x, self.fc1, self.bn1, self._fc_cache.setdefault(1, {}))
+            x = linear_bn(x, self.fc2, self.bn2, self._fc_cache.setdefault(2, {}))
+        else:
+            x = F.relu(self.bn1(self.fc1(x)))
+            x = F.relu(self.bn2(self.dropout(self.fc2(x))))
         x = F.log_softmax(self.fc3(x), dim=1)
         return x, trans_feat, x.data.max(1)[1]
 
@@ -110,7 +125,7 @@ class RotationV1(_ConvStack):
     def forward(self, x):
         mode = self._mode(x)
         h, _ = self._split_ftnet(x, mode)
-        return self._tail(self._layers(h, 2, len(self.conv), True, mode, rows=mode != "torch"))
+        return self._tail(self._layers(h, 2, len(self.conv), True, mode, rows=mode != "torch"), mode)
 
 
 class TranslationV1(_ConvStack):
@@ -128,7 +143,8 @@ class TranslationV1(_ConvStack):
     def forward(self, x, mean):
         if self.mean_mlp == 'True':
             mean = self.fc2(F.relu(self.bn1(self.fc1(mean))))
-        return self._tail(self._layers(x, 0, len(self.conv), True, self._mode(x))) + mean
+        mode = self._mode(x)
+        return self._tail(self._layers(x, 0, len(self.conv), True, mode), mode) + mean
 
 
 class SignV1(_ConvStack):
@@ -138,7 +154,8 @@ class SignV1(_ConvStack):
         self.dropout = nn.Dropout(p=0.4)
 
     def forward(self, x):
-        x = torch.sigmoid(self._tail(self._layers(x, 0, len(self.conv), True, self._mode(x))))
+        mode = self._mode(x)
+        x = torch.sigmoid(self._tail(self._layers(x, 0, len(self.conv), True, mode), mode))
         return x, torch.sign(x - 0.5)
 
 
@@ -150,7 +167,8 @@ class WidthV1(_ConvStack):
         self.dropout = nn.Dropout(p=0.4)
 
     def forward(self, x):
-        return self._tail(self._layers(x, 0, len(self.conv), True, self._mode(x)))
+        mode = self._mode(x)
+        return self._tail(self._layers(x, 0, len(self.conv), True, mode), mode)
 
 
 class PoseV1(_ConvStack):
@@ -196,7 +214,7 @@ class PoseV1(_ConvStack):
             x = self._layers(h, 2, len(self.conv), True, mode, rows=mode != "torch")
         else:
             x = self._layers(x, 0, len(self.conv), True, mode)
-        x = self._tail(x)
+        x = self._tail(x, mode)
         if self.mean:
             mean = torch.mean(x[:, :3, :], dim=2)
             mean = self.fc2(F.relu(self.bn1(self.fc1(mean))))

@@ -119,6 +119,54 @@ def run_mlp(mode, x, convs, bns, cache, pool=True, last_relu=True, module=None, 
     return point_mlp(x, convs, bns, cache, pool, last_relu, module, rows)
 
 
+def _fold_linear(fc, bn, cache, extra=None):
+    """Linear + eval BatchNorm1d folded into one (W', b') in float64, then float32:
+    W' = a*W, b' = a*(b - running_mean) + beta (+ extra), a = gamma / sqrt(running_var + eps).
+    Cached until a parameter or buffer changes.  None when bn normalises with batch statistics
+    (no running stats), which cannot fold."""
+    tensors = [fc.weight, fc.bias]
+    if bn is not None:
+        if bn.running_mean is None or bn.running_var is None:
+            return None
+        tensors += [bn.weight, bn.bias, bn.running_mean, bn.running_var]
+    if extra is not None:
+        tensors.append(extra)
+    key = tuple((t.data_ptr(), t._version) for t in tensors if t is not None)
+    if cache.get("key") != key:
+        with torch.no_grad():
+            W = fc.weight.double()
+            b = fc.bias.double() if fc.bias is not None else torch.zeros(W.shape[0], dtype=torch.float64,
+                                                                         device=W.device)
+            if bn is not None:
+                a = torch.rsqrt(bn.running_var.double() + bn.eps)
+                if bn.weight is not None:
+                    a = a * bn.weight.double()
+                W = W * a[:, None]
+                b = (b - bn.running_mean.double()) * a
+                if bn.bias is not None:
+                    b = b + bn.bias.double()
+            if extra is not None:
+                b = b + extra.double().reshape(-1)
+            cache["key"] = key
+            cache["wb"] = (W.float().contiguous(), b.float().contiguous())
+    return cache["wb"]
+
+
+def linear_bn(x, fc, bn, cache, relu=True, extra=None):
+    """Eval-mode ``relu(bn(fc(x)))`` (``bn`` may be None; ``extra`` a bias added after) as one
+    folded library GEMM + an in-place ReLU: the v1 FC tails (pointnet_utils.py:36-40, the heads'
+    fc / bn_fc) on B rows are launch-bound, and BatchNorm1d's eval kernels cost more than the
+    GEMM.  Falls back to the modules when the BN cannot fold."""
+    wb = _fold_linear(fc, bn, cache, extra)
+    if wb is None:
+        y = bn(fc(x)) if bn is not None else fc(x)
+        if extra is not None:
+            y = y + extra
+        return F.relu(y) if relu else y
+    y = F.linear(x, wb[0], wb[1])
+    return y.relu_() if relu else y
+
+
 def _rows_to_cf(rows):
     """[B, N, C] rows -> the reference's channel-first [B, C, N] view (no copy)."""
     return rows.permute(0, 2, 1)
@@ -150,6 +198,7 @@ class _TNet(nn.Module):
         self.bn5 = nn.BatchNorm1d(256)
         self._k = k
         self._cache = {}
+        self._fc_cache = {}
         # the reference rebuilds eye(k) from numpy and copies it to the device every forward
         # (pointnet_utils.py:37-40); here it is a non-persistent buffer (state_dict unchanged)
         # that moves with the module, so the forward has no host copy and captures in a graph
@@ -168,6 +217,11 @@ class _TNet(nn.Module):
             g = torch.max(h, 2, keepdim=True)[0].view(-1, 1024)
         else:
             g = run_mlp(mode, x, convs, bns, self._cache, module=self)
+        if mode == "fused":  # FC + BN folded, the identity in fc3's bias
+            g = linear_bn(g, self.fc1, self.bn4, self._fc_cache.setdefault(1, {}))
+            g = linear_bn(g, self.fc2, self.bn5, self._fc_cache.setdefault(2, {}))
+            g = linear_bn(g, self.fc3, None, self._fc_cache.setdefault(3, {}), relu=False, extra=self._iden)
+            return g.view(-1, self._k, self._k)
         g = F.relu(self.bn4(self.fc1(g)))
         g = F.relu(self.bn5(self.fc2(g)))
         g = self.fc3(g)
@@ -246,4 +300,4 @@ def feature_transform_reguliarzer(transform):
 
 
 __all__ = ["TNet3d", "TNetkd", "PointNetEncoder", "feature_transform_reguliarzer", "point_mlp",
-           "mlp_mode", "run_mlp"]
+           "mlp_mode", "run_mlp", "linear_bn"]

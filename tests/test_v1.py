@@ -206,3 +206,36 @@ def test_point_mlp_channel_first_source(C, N, pool, tview):
         ref = _torch_layers(x, convs, bns)
         ref = ref.max(2)[0] if pool else ref.permute(0, 2, 1)
     assert_close(got.cpu().numpy(), ref.cpu().numpy(), 1e-5)
+
+
+@pytest.mark.parametrize("relu,affine,extra", [(True, True, False), (False, True, True), (True, False, False)])
+def test_linear_bn_folds_eval_batchnorm(relu, affine, extra):
+    """linear_bn (the eval FC tails: Linear + BatchNorm1d folded into one GEMM) against the
+    modules; plain torch, so it is checked on the CPU.  A BN without running statistics (batch
+    statistics even in eval) is not folded: the modules run."""
+    from pn2.pointnet_utils import linear_bn
+    torch.manual_seed(5)
+    fc = torch.nn.Linear(256, 128)
+    bn = torch.nn.BatchNorm1d(128, affine=affine)
+    cases.randomize_bn(bn, 9) if affine else None
+    with torch.no_grad():
+        bn.running_mean.uniform_(-0.1, 0.1)
+        bn.running_var.uniform_(0.5, 1.5)
+    bn.eval()
+    x = torch.randn(8, 256)
+    e = torch.randn(1, 128) if extra else None
+    cache = {}
+    with torch.no_grad():
+        got = linear_bn(x, fc, bn, cache, relu=relu, extra=e)
+        ref = bn(fc(x)) + (e if extra else 0)
+        ref = torch.relu(ref) if relu else ref
+        assert_close(got.numpy(), ref.numpy(), 1e-5)
+        fc.weight.mul_(2)  # a parameter change invalidates the folded copy
+        got = linear_bn(x, fc, bn, cache, relu=relu, extra=e)
+        ref = bn(fc(x)) + (e if extra else 0)
+        ref = torch.relu(ref) if relu else ref
+        assert_close(got.numpy(), ref.numpy(), 1e-5)
+        nostats = torch.nn.BatchNorm1d(128, track_running_stats=False).eval()
+        got = linear_bn(x, fc, nostats, {}, relu=relu)
+        ref = nostats(fc(x))
+        assert_close(got.numpy(), (torch.relu(ref) if relu else ref).numpy(), 1e-6)
