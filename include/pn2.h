@@ -51,7 +51,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 7
+#define PN2_ABI_VERSION 8
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -251,6 +251,15 @@ int pn2_bn_relu_backward_f32(const float *Y, int64_t M, int64_t C, int64_t ld, c
                              const int32_t *arg, int64_t K, const double *sxhat, float *dY,
                              int64_t ldy, float *dgamma, float *dbeta, float *dbias, void *ws,
                              int64_t ws_bytes, int flags, void *stream);
+
+/* ---- small-batch fully connected layer (the v1 FC tails, eval BN folded into W / bias on the
+ * host): out[b*ldo + n] = act(sum_k x[b*ldx + k] * W[n*K + k] + bias[n]) for b < B <= 16,
+ * W row-major [N][K], bias may be NULL; flags PN2_LINEAR_RELU applies the ReLU.  Float32 FMA.
+ * Reference: pointnet_utils.py:36-40, pointnet_cls.py:18-27, rotation.py:45-49. ---- */
+#define PN2_LINEAR_RELU 1
+int pn2_linear_rows_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const float *W,
+                        const float *bias, float *out, int64_t ldo, int64_t N, int flags,
+                        void *stream);
 
 /* Which kernel family served this thread's last successful pn2_sa_mlp_max_* call:
  * PN2_PATH_F32 (fp32 MFMA kernels), PN2_PATH_SPLIT_BF16 (split-bf16 chain / dense kernels) or

@@ -1,0 +1,151 @@
+// linear.hip -- small-batch fully connected layer: out = act(x W^T + bias) for B <= 16 rows.
+//
+// Reference: the FC tails of the PointNet-v1 networks, /root/reference/model/pointnet_utils.py:
+// 36-40 (T-Net fc1-fc3 + bn4/bn5), pointnet_cls.py:18-27 and the v1 heads' fc / bn_fc stacks
+// (rotation.py:45-49), with each eval BatchNorm1d folded into W and bias on the host
+// (pn2/pointnet_utils.py linear_bn).  At B <= 16 rows these are matrix-vector products:
+// the weight (up to 1024 x 4096 floats) is read once, so the bound is HBM bytes of W -- and in
+// practice the launch: the library GEMMs chosen for these shapes run 5-13 us each, several
+// times the weight's read time.
+//
+// Layout: one wave per kLinRows (4 or 2 by the row count) consecutive output features; each
+// lane walks K with 16-byte loads of the W rows (coalesced: a wave reads 1 KB of a row per step) and of the x rows (L2
+// resident: x is at most 16 x K floats), accumulating kLinRows x B partial dot products in
+// registers, then a transpose-reduce across the wave (32 shuffles for the 32 sums).  Float32
+// FMA throughout (the library GEMM's arithmetic; the summation order differs, as between any
+// two GEMM kernels).  Measured per call in a graph (tools/debug/fc_shapes.py), B = 8:
+// 1024->512 5.8 us (library + ReLU 7.6), 512->256 4.3 (12.7), 256->9 3.1 (4.8), 256->4096 3.8
+// (5.9); above 16 rows the library GEMM is faster and pn2 uses it.
+#include "pn2_internal.h"
+
+namespace pn2 {
+
+constexpr int kLinWaves = 4;   // waves per workgroup
+
+// output features per wave: kLinRows x BT accumulators stay within ~128 VGPRs
+template <int BT>
+constexpr int lin_rows() { return BT <= 8 ? 4 : 2; }
+
+// one transpose-reduce step over lane bit 2H: keep H of the 2H values, add the partner's copy
+// (H is a template parameter so every register index is static)
+template <int H>
+__device__ __forceinline__ void lin_reduce_step(float *a, int lane) {
+    const bool up = (lane & (2 * H)) != 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        const float send = up ? a[i] : a[i + H];
+        const float keep = up ? a[i + H] : a[i];
+        a[i] = keep + __shfl_xor(send, 2 * H);
+    }
+}
+
+template <int BT>
+__global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float *__restrict__ x, int64_t ldx,
+                                                                     int B, int64_t K,
+                                                                     const float *__restrict__ W,
+                                                                     const float *__restrict__ bias,
+                                                                     float *__restrict__ out, int64_t ldo,
+                                                                     int64_t N, int relu, int vec) {
+    constexpr int kLinRows = lin_rows<BT>();
+    const int lane = threadIdx.x & 63;
+    const int64_t o0 = ((int64_t)blockIdx.x * kLinWaves + threadIdx.x / 64) * kLinRows;
+    if (o0 >= N) return;  // whole waves leave together
+    float acc[kLinRows][BT];
+#pragma unroll
+    for (int r = 0; r < kLinRows; ++r)
+#pragma unroll
+        for (int b = 0; b < BT; ++b) acc[r][b] = 0.f;
+    // row pointers clamped into range instead of guarded: every load of an iteration issues
+    // back to back (a branch per row made each wait for the previous one); the rows past B or N
+    // accumulate duplicates that are never stored
+    const float *wr[kLinRows];
+#pragma unroll
+    for (int r = 0; r < kLinRows; ++r) wr[r] = W + (o0 + r < N ? o0 + r : N - 1) * K;
+    const float *xr[BT];
+#pragma unroll
+    for (int b = 0; b < BT; ++b) xr[b] = x + (int64_t)(b < B ? b : B - 1) * ldx;
+    if (vec) {  // 16-byte aligned rows (host-checked)
+        for (int64_t k = (int64_t)lane * 4; k < K; k += 256) {
+            float4 w[kLinRows], v[BT];
+#pragma unroll
+            for (int r = 0; r < kLinRows; ++r) w[r] = *reinterpret_cast<const float4 *>(wr[r] + k);
+#pragma unroll
+            for (int b = 0; b < BT; ++b) v[b] = *reinterpret_cast<const float4 *>(xr[b] + k);
+#pragma unroll
+            for (int b = 0; b < BT; ++b) {
+#pragma unroll
+                for (int r = 0; r < kLinRows; ++r) {
+                    float a = acc[r][b];
+                    a = fmaf(w[r].x, v[b].x, a);
+                    a = fmaf(w[r].y, v[b].y, a);
+                    a = fmaf(w[r].z, v[b].z, a);
+                    a = fmaf(w[r].w, v[b].w, a);
+                    acc[r][b] = a;
+                }
+            }
+        }
+    } else {
+        for (int64_t k = lane; k < K; k += 64) {
+            float w[kLinRows], v[BT];
+#pragma unroll
+            for (int r = 0; r < kLinRows; ++r) w[r] = wr[r][k];
+#pragma unroll
+            for (int b = 0; b < BT; ++b) v[b] = xr[b][k];
+#pragma unroll
+            for (int b = 0; b < BT; ++b)
+#pragma unroll
+                for (int r = 0; r < kLinRows; ++r) acc[r][b] = fmaf(w[r], v[b], acc[r][b]);
+        }
+    }
+    // transpose-reduce: kLinRows x BT = 32 partial sums per lane.  Each xor step keeps half
+    // of the values and adds the partner lane's copy of that half (one shuffle per kept value:
+    // 16 + 8 + 4 + 2 + 1 + 1 = 32 shuffles, not 32 x 6); lane L ends with value (L >> 1) & 31
+    static_assert(kLinRows * BT == 32, "32 values per lane");
+    float a[32];
+#pragma unroll
+    for (int r = 0; r < kLinRows; ++r)
+#pragma unroll
+        for (int b = 0; b < BT; ++b) a[r * BT + b] = acc[r][b];
+    lin_reduce_step<16>(a, lane);
+    lin_reduce_step<8>(a, lane);
+    lin_reduce_step<4>(a, lane);
+    lin_reduce_step<2>(a, lane);
+    lin_reduce_step<1>(a, lane);
+    a[0] += __shfl_xor(a[0], 1);
+    const int v = (lane >> 1) & 31, r = v / BT, b = v % BT;
+    if ((lane & 1) == 0 && b < B && o0 + r < N) {
+        const float y = a[0] + (bias ? bias[o0 + r] : 0.f);
+        out[b * ldo + o0 + r] = relu ? (y > 0.f ? y : 0.f) : y;
+    }
+}
+
+}  // namespace pn2
+
+using namespace pn2;
+
+extern "C" int pn2_linear_rows_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const float *W,
+                                   const float *bias, float *out, int64_t ldo, int64_t N, int flags,
+                                   void *stream) {
+    PN2_REQUIRE(x && W && out, "pn2_linear_rows_f32: null pointer");
+    PN2_REQUIRE(B >= 1 && B <= 16 && K >= 1 && N >= 1 && ldx >= K && ldo >= N,
+                "pn2_linear_rows_f32: bad shape (1 <= B <= 16)");
+    PN2_REQUIRE((flags & ~PN2_LINEAR_RELU) == 0, "pn2_linear_rows_f32: unknown flags");
+    // 16-byte loads when every row start is 16-byte aligned, else the scalar path
+    const int vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) == 0 &&
+                    (K & 3) == 0 && (ldx & 3) == 0;
+    const int relu = (flags & PN2_LINEAR_RELU) ? 1 : 0;
+    hipStream_t st = as_stream(stream);
+    auto grid = [N](int rows) {
+        const int64_t waves = (N + rows - 1) / rows;
+        return dim3((unsigned)((waves + kLinWaves - 1) / kLinWaves));
+    };
+    const dim3 block(64 * kLinWaves);
+    if (B <= 8)
+        hipLaunchKernelGGL(linear_rows_kernel<8>, grid(lin_rows<8>()), block, 0, st, x, ldx, (int)B, K, W, bias,
+                           out, ldo, N, relu, vec);
+    else
+        hipLaunchKernelGGL(linear_rows_kernel<16>, grid(lin_rows<16>()), block, 0, st, x, ldx, (int)B, K, W, bias,
+                           out, ldo, N, relu, vec);
+    PN2_LAUNCH_CHECK("linear_rows_kernel");
+    return PN2_OK;
+}

@@ -50,6 +50,7 @@ PATH_F32 = 1
 PATH_SPLIT_BF16 = 2
 PATH_BF16 = 3
 LAYER_NO_RELU = 1
+LINEAR_RELU = 1
 
 # name -> (restype, argtypes); every symbol include/pn2.h declares
 SIGNATURES = {
@@ -78,6 +79,7 @@ SIGNATURES = {
                                      _vp]),
     "pn2_bn_train_forward_f32": (_int, [_vp, _i64, _i64, _i64, ctypes.c_double, ctypes.c_double, _vp,
                                         _vp, _vp, _vp, _vp, _i64, _int, _vp, _vp, _vp, _i64, _vp]),
+    "pn2_linear_rows_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _i64, _int, _vp]),
     "pn2_group_max_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp]),
     "pn2_bn_relu_backward_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
                                         _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64,
@@ -93,7 +95,7 @@ SIGNATURES = {
                                    _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _lib = None
 
 

@@ -432,3 +432,24 @@ sa_mlp_max_ = torch.library.custom_op("pn2::sa_mlp_max_", sa_mlp_max_direct, mut
 def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits, precision="fp32",
       flags=None, rows=None, pool=True):
     return None
+
+
+LINEAR_ROWS_MAX = 16  # above this the library GEMM is faster (tools/debug/fc_shapes.py)
+
+
+def linear_rows(x: Tensor, weight: Tensor, bias: Optional[Tensor], relu: bool) -> Tensor:
+    """act(x @ weight^T + bias) for a few rows (B <= LINEAR_ROWS_MAX) on pn2_linear_rows_f32:
+    x [B, K] (unit column stride), weight [N, K] contiguous, bias [N] or None -> [B, N]."""
+    _dev(x, "pn2::linear_rows")
+    B, K = x.shape
+    N = weight.shape[0]
+    if B < 1 or B > LINEAR_ROWS_MAX or x.stride(1) != 1 or not weight.is_contiguous() or \
+            weight.shape[1] != K or (bias is not None and not bias.is_contiguous()):
+        raise ValueError("pn2::linear_rows: x [B<=16, K] with unit column stride, weight [N, K] "
+                         "contiguous")
+    out = torch.empty(B, N, device=x.device, dtype=torch.float32)
+    check(_L.pn2_linear_rows_f32(x.data_ptr(), x.stride(0), B, K, weight.data_ptr(),
+                                 0 if bias is None else bias.data_ptr(), out.data_ptr(), N, N,
+                                 _lib.LINEAR_RELU if relu else 0, _stream(x)),
+          "pn2_linear_rows_f32")
+    return out

@@ -239,3 +239,25 @@ def test_linear_bn_folds_eval_batchnorm(relu, affine, extra):
         got = linear_bn(x, fc, nostats, {}, relu=relu)
         ref = nostats(fc(x))
         assert_close(got.numpy(), (torch.relu(ref) if relu else ref).numpy(), 1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,K,N,relu", [(8, 1024, 512, True), (8, 512, 256, True), (8, 256, 9, False),
+                                        (8, 256, 4096, False), (3, 1024, 7, True), (16, 512, 130, True),
+                                        (16, 1024, 512, True), (5, 6, 3, False), (12, 255, 33, True)])
+def test_linear_rows_matches_torch(B, K, N, relu):
+    """pn2_linear_rows_f32 (the small-batch FC kernel: 16-byte and scalar paths, 1/2/4 output
+    features per wave) against float64 torch, fp32 tolerance."""
+    from pn2 import ops
+    torch.manual_seed(B * K + N)
+    x = torch.randn(B, K, device="cuda")
+    W = torch.randn(N, K, device="cuda") / K ** 0.5
+    b = torch.randn(N, device="cuda")
+    got = ops.linear_rows(x, W, b, relu)
+    ref = x.double() @ W.double().t() + b.double()
+    ref = ref.clamp_min(0) if relu else ref
+    assert_close(got.cpu().numpy(), ref.cpu().numpy(), 2e-6)
+    xs = torch.randn(B, K + 3, device="cuda")[:, 1:K + 1]  # strided rows, misaligned base
+    got = ops.linear_rows(xs, W, None, False)
+    ref = xs.double() @ W.double().t()
+    assert_close(got.cpu().numpy(), ref.cpu().numpy(), 2e-6)
