@@ -252,8 +252,9 @@ int pn2_bn_relu_backward_f32(const float *Y, int64_t M, int64_t C, int64_t ld, c
                              int64_t ldy, float *dgamma, float *dbeta, float *dbias, void *ws,
                              int64_t ws_bytes, int flags, void *stream);
 
-/* ---- small-batch fully connected layer (the v1 FC tails, eval BN folded into W / bias on the
- * host): out[b*ldo + n] = act(sum_k x[b*ldx + k] * W[n*K + k] + bias[n]) for b < B <= 16,
+/* ---- small-batch fully connected layer (the eval FC tails, BN folded into W / bias on the
+ * host): out[b*ldo + n] = act(sum_k x[b*ldx + k] * W[n*K + k] + bias[n]) for b < B (rows in
+ * blocks of 16; each element computed the same way whatever B is),
  * W row-major [N][K], bias may be NULL; flags PN2_LINEAR_RELU applies the ReLU.  Float32 FMA.
  * Reference: pointnet_utils.py:36-40, pointnet_cls.py:18-27, rotation.py:45-49. ---- */
 #define PN2_LINEAR_RELU 1

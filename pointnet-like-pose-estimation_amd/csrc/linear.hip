@@ -1,9 +1,10 @@
-// linear.hip -- small-batch fully connected layer: out = act(x W^T + bias) for B <= 16 rows.
+// linear.hip -- small-batch fully connected layer: out = act(x W^T + bias), rows in blocks of
+// 16.
 //
 // Reference: the FC tails of the PointNet-v1 networks, /root/reference/model/pointnet_utils.py:
 // 36-40 (T-Net fc1-fc3 + bn4/bn5), pointnet_cls.py:18-27 and the v1 heads' fc / bn_fc stacks
 // (rotation.py:45-49), with each eval BatchNorm1d folded into W and bias on the host
-// (pn2/pointnet_utils.py linear_bn).  At B <= 16 rows these are matrix-vector products:
+// (pn2/pointnet_utils.py linear_bn).  At a few rows these are matrix-vector products:
 // the weight (up to 1024 x 4096 floats) is read once, so the bound is HBM bytes of W -- and in
 // practice the launch: the library GEMMs chosen for these shapes run 5-13 us each, several
 // times the weight's read time.
@@ -15,7 +16,7 @@
 // FMA throughout (the library GEMM's arithmetic; the summation order differs, as between any
 // two GEMM kernels).  Measured per call in a graph (tools/debug/fc_shapes.py), B = 8:
 // 1024->512 5.8 us (library + ReLU 7.6), 512->256 4.3 (12.7), 256->9 3.1 (4.8), 256->4096 3.8
-// (5.9); above 16 rows the library GEMM is faster and pn2 uses it.
+// (5.9).  More rows run as blocks of 16 (grid.y).
 #include "pn2_internal.h"
 
 namespace pn2 {
@@ -48,6 +49,12 @@ __global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float
                                                                      int64_t N, int relu, int vec) {
     constexpr int kLinRows = lin_rows<BT>();
     const int lane = threadIdx.x & 63;
+    // row block blockIdx.y: every output element is computed the same way whatever B is (the
+    // per-lane FMA order depends on k only, the reduction tree on the lane only), so a batch
+    // split into shards gives bit-identical rows
+    x += (int64_t)blockIdx.y * BT * ldx;
+    out += (int64_t)blockIdx.y * BT * ldo;
+    B = B - (int)blockIdx.y * BT < BT ? B - (int)blockIdx.y * BT : BT;
     const int64_t o0 = ((int64_t)blockIdx.x * kLinWaves + threadIdx.x / 64) * kLinRows;
     if (o0 >= N) return;  // whole waves leave together
     float acc[kLinRows][BT];
@@ -127,24 +134,24 @@ extern "C" int pn2_linear_rows_f32(const float *x, int64_t ldx, int64_t B, int64
                                    const float *bias, float *out, int64_t ldo, int64_t N, int flags,
                                    void *stream) {
     PN2_REQUIRE(x && W && out, "pn2_linear_rows_f32: null pointer");
-    PN2_REQUIRE(B >= 1 && B <= 16 && K >= 1 && N >= 1 && ldx >= K && ldo >= N,
-                "pn2_linear_rows_f32: bad shape (1 <= B <= 16)");
+    PN2_REQUIRE(B >= 1 && (B + 15) / 16 <= 65535 && K >= 1 && N >= 1 && ldx >= K && ldo >= N,
+                "pn2_linear_rows_f32: bad shape");
     PN2_REQUIRE((flags & ~PN2_LINEAR_RELU) == 0, "pn2_linear_rows_f32: unknown flags");
     // 16-byte loads when every row start is 16-byte aligned, else the scalar path
     const int vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) == 0 &&
                     (K & 3) == 0 && (ldx & 3) == 0;
     const int relu = (flags & PN2_LINEAR_RELU) ? 1 : 0;
     hipStream_t st = as_stream(stream);
-    auto grid = [N](int rows) {
+    auto grid = [N, B](int rows, int bt) {
         const int64_t waves = (N + rows - 1) / rows;
-        return dim3((unsigned)((waves + kLinWaves - 1) / kLinWaves));
+        return dim3((unsigned)((waves + kLinWaves - 1) / kLinWaves), (unsigned)((B + bt - 1) / bt));
     };
     const dim3 block(64 * kLinWaves);
     if (B <= 8)
-        hipLaunchKernelGGL(linear_rows_kernel<8>, grid(lin_rows<8>()), block, 0, st, x, ldx, (int)B, K, W, bias,
+        hipLaunchKernelGGL(linear_rows_kernel<8>, grid(lin_rows<8>(), 8), block, 0, st, x, ldx, (int)B, K, W, bias,
                            out, ldo, N, relu, vec);
     else
-        hipLaunchKernelGGL(linear_rows_kernel<16>, grid(lin_rows<16>()), block, 0, st, x, ldx, (int)B, K, W, bias,
+        hipLaunchKernelGGL(linear_rows_kernel<16>, grid(lin_rows<16>(), 16), block, 0, st, x, ldx, (int)B, K, W, bias,
                            out, ldo, N, relu, vec);
     PN2_LAUNCH_CHECK("linear_rows_kernel");
     return PN2_OK;

@@ -21,12 +21,20 @@ import torch.nn.functional as F
 
 from .pointnet2_utils import PointNetSetAbstraction as SA
 from .pointnet2_utils import PointNetSetAbstractionMsg as SAMsg
+from .pointnet2_utils import _needs_autograd
+from .pointnet_utils import linear_bn
 
 
 class _FCHead(nn.Module):
-    """fc1/bn1/relu/drop -> fc2/bn2/relu/drop -> fc3, shared by every head."""
+    """fc1/bn1/relu/drop -> fc2/bn2/relu/drop -> fc3, shared by every head.  Eval without
+    autograd: each fc + bn folded into one GEMM with the ReLU (pn2.pointnet_utils.linear_bn;
+    dropout is the identity in eval)."""
 
     def _fc(self, x):
+        if not _needs_autograd(self, x):
+            x = linear_bn(x, self.fc1, self.bn1, self._fc_cache.setdefault(1, {}))
+            x = linear_bn(x, self.fc2, self.bn2, self._fc_cache.setdefault(2, {}))
+            return self.fc3(x)
         x = self.drop(F.relu(self.bn1(self.fc1(x))))
         x = self.drop(F.relu(self.bn2(self.fc2(x))))
         return self.fc3(x)
@@ -38,6 +46,7 @@ class _FCHead(nn.Module):
         self.drop = nn.Dropout(0.4)
         self.bn1 = nn.BatchNorm1d(512)
         self.bn2 = nn.BatchNorm1d(256)
+        self._fc_cache = {}
 
 
 class ClsSSG(_FCHead):

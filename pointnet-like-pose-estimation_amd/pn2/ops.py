@@ -434,18 +434,16 @@ def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits
     return None
 
 
-LINEAR_ROWS_MAX = 16  # above this the library GEMM is faster (tools/debug/fc_shapes.py)
-
-
 def linear_rows(x: Tensor, weight: Tensor, bias: Optional[Tensor], relu: bool) -> Tensor:
-    """act(x @ weight^T + bias) for a few rows (B <= LINEAR_ROWS_MAX) on pn2_linear_rows_f32:
+    """act(x @ weight^T + bias) on pn2_linear_rows_f32 (rows in blocks of 16; each output
+    element computed the same way whatever the row count, so batch shards are bit-identical):
     x [B, K] (unit column stride), weight [N, K] contiguous, bias [N] or None -> [B, N]."""
     _dev(x, "pn2::linear_rows")
     B, K = x.shape
     N = weight.shape[0]
-    if B < 1 or B > LINEAR_ROWS_MAX or x.stride(1) != 1 or not weight.is_contiguous() or \
+    if B < 1 or x.stride(1) != 1 or not weight.is_contiguous() or \
             weight.shape[1] != K or (bias is not None and not bias.is_contiguous()):
-        raise ValueError("pn2::linear_rows: x [B<=16, K] with unit column stride, weight [N, K] "
+        raise ValueError("pn2::linear_rows: x [B, K] with unit column stride, weight [N, K] "
                          "contiguous")
     out = torch.empty(B, N, device=x.device, dtype=torch.float32)
     check(_L.pn2_linear_rows_f32(x.data_ptr(), x.stride(0), B, K, weight.data_ptr(),

@@ -156,16 +156,16 @@ def linear_bn(x, fc, bn, cache, relu=True, extra=None):
     """Eval-mode ``relu(bn(fc(x)))`` (``bn`` may be None; ``extra`` a bias added after) as one
     folded GEMM with the ReLU in its epilogue: the v1 FC tails (pointnet_utils.py:36-40, the
     heads' fc / bn_fc) on B rows are launch-bound, and BatchNorm1d's eval kernels cost more than
-    the GEMM.  Device tensors of <= 32 rows run on pn2_linear_rows_f32 (the library GEMMs picked
-    for these shapes take 7-12 us); more rows (and CPU tensors, in tests) on F.linear.  Falls
-    back to the modules when the BN cannot fold."""
+    the GEMM.  Device tensors run on pn2_linear_rows_f32 (the library GEMMs picked for these
+    shapes take 5-13 us; CPU tensors, in tests, on F.linear).  Falls back to the modules when
+    the BN cannot fold."""
     wb = _fold_linear(fc, bn, cache, extra)
     if wb is None:
         y = bn(fc(x)) if bn is not None else fc(x)
         if extra is not None:
             y = y + extra
         return F.relu(y) if relu else y
-    if x.is_cuda and x.dim() == 2 and x.shape[0] <= ops.LINEAR_ROWS_MAX and x.stride(1) == 1:
+    if x.is_cuda and x.dim() == 2 and x.shape[0] >= 1 and x.stride(1) == 1:
         return ops.linear_rows(x, wb[0], wb[1], relu)
     y = F.linear(x, wb[0], wb[1])
     return y.relu_() if relu else y

@@ -244,10 +244,12 @@ def test_linear_bn_folds_eval_batchnorm(relu, affine, extra):
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,K,N,relu", [(8, 1024, 512, True), (8, 512, 256, True), (8, 256, 9, False),
                                         (8, 256, 4096, False), (3, 1024, 7, True), (16, 512, 130, True),
-                                        (16, 1024, 512, True), (5, 6, 3, False), (12, 255, 33, True)])
+                                        (16, 1024, 512, True), (5, 6, 3, False), (12, 255, 33, True),
+                                        (32, 1024, 512, True), (70, 300, 40, False)])
 def test_linear_rows_matches_torch(B, K, N, relu):
-    """pn2_linear_rows_f32 (the small-batch FC kernel: 16-byte and scalar paths, 1/2/4 output
-    features per wave) against float64 torch, fp32 tolerance."""
+    """pn2_linear_rows_f32 (the small-batch FC kernel: 16-byte and scalar paths, 2/4 output
+    features per wave, row blocks of 16) against float64 torch, fp32 tolerance; every row
+    bit-identical to the same row computed in a batch of its own (batch sharding)."""
     from pn2 import ops
     torch.manual_seed(B * K + N)
     x = torch.randn(B, K, device="cuda")
@@ -257,6 +259,8 @@ def test_linear_rows_matches_torch(B, K, N, relu):
     ref = x.double() @ W.double().t() + b.double()
     ref = ref.clamp_min(0) if relu else ref
     assert_close(got.cpu().numpy(), ref.cpu().numpy(), 2e-6)
+    one = torch.cat([ops.linear_rows(x[i:i + 1], W, b, relu) for i in range(B)])
+    np.testing.assert_array_equal(one.cpu().numpy(), got.cpu().numpy())
     xs = torch.randn(B, K + 3, device="cuda")[:, 1:K + 1]  # strided rows, misaligned base
     got = ops.linear_rows(xs, W, None, False)
     ref = xs.double() @ W.double().t()

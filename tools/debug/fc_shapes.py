@@ -32,7 +32,7 @@ def graph_us(fn, reps=50):
     return round(e0.elapsed_time(e1) / (10 * reps) * 1e3, 2)
 
 
-for B in [int(v) for v in os.environ.get("BS", "8,32").split(",")]:
+for B in [int(v) for v in os.environ.get("BS", "8,16,32").split(",")]:
     for K, N in ((1024, 512), (512, 256), (256, 9), (256, 4096)):
         x = torch.randn(B, K, device="cuda")
         W = torch.randn(N, K, device="cuda")
