@@ -159,8 +159,8 @@ def linear_bn(x, fc, bn, cache, relu=True, extra=None):
     the GEMM.  Device tensors run on pn2_linear_rows_f32 (the library GEMMs picked for these
     shapes take 5-13 us; CPU tensors, in tests, on F.linear).  Falls back to the modules when
     the BN cannot fold."""
-    wb = _fold_linear(fc, bn, cache, extra)
-    if wb is None:
+    wb = _fold_linear(fc, bn, cache, extra) if x.dtype == torch.float32 else None
+    if wb is None:  # BN without running statistics, or a non-float32 model: the modules
         y = bn(fc(x)) if bn is not None else fc(x)
         if extra is not None:
             y = y + extra
