@@ -168,22 +168,62 @@ class PipelinedForward:
         the ball query of each radius -- both read only coordinates, so a batch's whole
         geometry runs ahead of its MLPs.  A group_all layer ends a head's chain; an SA layer
         after it starts the next head's chain from the input again (a model holding several
-        heads over the same cloud, e.g. MultiHead(rotation_ssg, translation_ssg))."""
-        entries = {}
-        pts = x.permute(0, 2, 1)
+        heads over the same cloud, e.g. MultiHead(rotation_ssg, translation_ssg)).
+
+        Several chains: their first layers all sample the input, so they run as ONE FPS launch
+        over the input repeated once per chain (each copy with its own start draws).  FPS is
+        latency-bound on one workgroup per cloud -- 16 clouds take as long as 8
+        (tools/debug/fps_batch_merge.py) -- so the heads' first FPS run side by side instead of
+        one after the other.  The copy keeps x's layout (the packed squared norms follow the
+        reference's layout-dependent summation order), and every start is still drawn in layer
+        order before any launch."""
+        B, _, N = x.shape
+        dev = x.device
+        chains, cur = [], []
         for sa in self.sas:
             if getattr(sa, "group_all", False):
-                pts = x.permute(0, 2, 1)
+                if cur:
+                    chains.append(cur)
+                cur = []
                 continue
-            B, N, C = pts.shape
-            _, newp, cpk, ppk = ops.fps_direct(pts, sa.point_number, shard.device_start(B, N, x.device))
-            if isinstance(sa, PointNetSetAbstractionMsg):
-                rk = list(zip(sa.radius_list, sa.sample_number_list))
-            else:
-                rk = [(sa.radius, sa.sample_number)]
-            idxs = [ops.ball_query_direct(ppk, cpk, C, r, k) for r, k in rk]
-            entries[id(sa)] = (pts.data_ptr(), newp, cpk, ppk, idxs)
-            pts = newp
+            cur.append(sa)
+        if cur:
+            chains.append(cur)
+        starts = {}  # drawn in layer order, as the eager forwards draw them
+        for ch in chains:
+            n = N
+            for sa in ch:
+                starts[id(sa)] = shard.device_start(B, n, dev)
+                n = sa.point_number
+        entries = {}
+        pts = x.permute(0, 2, 1)
+        first = {}  # chain -> (newp, cpk, ppk) of its first layer
+        heads = [ch[0] for ch in chains]
+        merge = len(chains) > 1 and len({sa.point_number for sa in heads}) == 1 and \
+            (pts.stride(2) == 1 or x.stride(2) == 1)
+        if merge:
+            k = len(chains)
+            # the same strides as pts: rows-contiguous stays rows, channel-first stays that
+            rep = torch.cat([pts] * k) if pts.stride(2) == 1 else torch.cat([x] * k).permute(0, 2, 1)
+            _, newp, cpk, ppk = ops.fps_direct(rep, heads[0].point_number,
+                                               torch.cat([starts[id(sa)] for sa in heads]))
+            for i, ch in enumerate(chains):
+                first[i] = (newp[i * B:(i + 1) * B], cpk[i * B:(i + 1) * B], ppk[i * B:(i + 1) * B])
+        for i, ch in enumerate(chains):
+            p = pts
+            for j, sa in enumerate(ch):
+                C = p.shape[2]
+                if j == 0 and i in first:
+                    newp, cpk, ppk = first[i]
+                else:
+                    _, newp, cpk, ppk = ops.fps_direct(p, sa.point_number, starts[id(sa)])
+                if isinstance(sa, PointNetSetAbstractionMsg):
+                    rk = list(zip(sa.radius_list, sa.sample_number_list))
+                else:
+                    rk = [(sa.radius, sa.sample_number)]
+                idxs = [ops.ball_query_direct(ppk, cpk, C, r, kk) for r, kk in rk]
+                entries[id(sa)] = (p.data_ptr(), newp, cpk, ppk, idxs)
+                p = newp
         return entries
 
     def run(self, batches, extras=None, post=None):
