@@ -382,11 +382,14 @@ def test_graphed_pipeline_matches_eager(head, tail):
             np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * float(np.abs(b).max()))
 
 
-def test_graphed_pipeline_multihead_matches_eager():
+@pytest.mark.parametrize("layout", ["contig", "tview"])
+def test_graphed_pipeline_multihead_matches_eager(layout):
     """BASELINE config 4 (rotation_ssg + translation_ssg over the same clouds) as one
     pn2.pipeline.MultiHead: the FPS chain covers both heads (a group_all layer ends a head's
-    chain, the next head restarts from the input), draws in the order separate eager calls take
-    them, and every output matches those calls (logits to 1e-6: head BLAS on another stream)."""
+    chain, the next head restarts from the input; the heads' first FPS run as one launch over
+    the repeated input), draws in the order separate eager calls take them, and every output
+    matches those calls (logits to 1e-6: head BLAS on another stream).  tview: the input is the
+    transpose view of [B, N, C] storage (the scripts' layout), which the repeated copy keeps."""
     from pn2 import heads as H
     from pn2 import shard
     from pn2.pipeline import GraphedPipeline, MultiHead
@@ -396,7 +399,10 @@ def test_graphed_pipeline_multihead_matches_eager():
     cases.randomize_bn(tra, 13)
     rot, tra = rot.to(DEV), tra.to(DEV)
     B, N = 8, 2048
-    xs = [cases.cloud("onehot10", B, N, 70 + i).permute(0, 2, 1).contiguous().to(DEV) for i in range(5)]
+    if layout == "tview":
+        xs = [cases.cloud("onehot10", B, N, 70 + i).to(DEV).permute(0, 2, 1) for i in range(5)]
+    else:
+        xs = [cases.cloud("onehot10", B, N, 70 + i).permute(0, 2, 1).contiguous().to(DEV) for i in range(5)]
     means = [(torch.randn(B, 3, generator=torch.Generator().manual_seed(i)).to(DEV),) for i in range(5)]
     torch.manual_seed(41)
     with torch.no_grad(), shard.batch_shard(4 * B, 2 * B):
