@@ -277,6 +277,42 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(
     }
 }
 
+// The same column sums when dA is scattered from the max (the last layer): dXn is nonzero only
+// on each group's argmax row, so S1 = sum_g mask * dOut[g][c] and S2 = sum_g mask * dOut[g][c] *
+// xhat(Y[g*K + arg[g][c]][c]) read G = M/K gathered rows instead of sweeping all M (K = 32-64 x
+// fewer bytes: the SA layers' widest Y, 268 MB at SSG, is the largest term of a training step).
+// Chunk blockIdx.y covers groups [y*chunk, y*chunk + chunk); partials as above.
+__global__ __launch_bounds__(256) void bn_bwd_partial_gather_kernel(
+    const float *__restrict__ Y, int64_t G, int64_t C, int64_t ld, const float *__restrict__ mean,
+    const float *__restrict__ invstd, const float *__restrict__ gamma, const float *__restrict__ beta,
+    const float *__restrict__ dOut, int64_t ldo, const int32_t *__restrict__ arg, int64_t K, int relu,
+    int64_t chunk, double *__restrict__ part) {
+    __shared__ double red[2][kTrLanes][kTrCols];
+    const int tx = threadIdx.x & (kTrCols - 1), ty = threadIdx.x / kTrCols;
+    const int64_t c = (int64_t)blockIdx.x * kTrCols + tx;
+    const int64_t g0 = (int64_t)blockIdx.y * chunk;
+    const int64_t g1 = g0 + chunk < G ? g0 + chunk : G;
+    double s1 = 0.0, s2 = 0.0;
+    if (c < C) {
+        const float mu = mean[c], is = invstd[c], ga = gamma[c], be = beta[c];
+        for (int64_t g = g0 + ty; g < g1; g += kTrLanes) {
+            const int64_t r = g * K + arg[g * C + c];
+            const float xh = tr_xhat(Y[r * ld + c], mu, is);
+            const float d = !relu || xh * ga + be > 0.f ? dOut[g * ldo + c] : 0.f;
+            s1 += (double)d;
+            s2 += (double)d * (double)xh;
+        }
+    }
+    red[0][ty][tx] = s1;
+    red[1][ty][tx] = s2;
+    __syncthreads();
+    if (ty == 0 && c < C) {
+        for (int l = 1; l < kTrLanes; ++l) s1 += red[0][l][tx], s2 += red[1][l][tx];
+        part[((int64_t)blockIdx.y * 2 + 0) * C + c] = s1;
+        part[((int64_t)blockIdx.y * 2 + 1) * C + c] = s2;
+    }
+}
+
 __global__ __launch_bounds__(64) void bn_bwd_final_kernel(const double *__restrict__ part, int64_t nch,
                                                           int64_t M, int64_t C, const float *__restrict__ gamma,
                                                           const float *__restrict__ invstd,
@@ -417,11 +453,23 @@ extern "C" int pn2_bn_relu_backward_f32(const float *Y, int64_t M, int64_t C, in
     hipStream_t st = as_stream(stream);
     double *part = static_cast<double *>(ws);
     double *sums = part + chunks(M, C) * 2 * C;
-    hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)chunks(M, C)),
-                       dim3(256), 0, st, Y, M, C, ld, mean, invstd, gamma, beta, dA, ldd, dOut, ldo, arg, K, relu,
-                       chunk_rows(M, C), part);
-    PN2_LAUNCH_CHECK("bn_bwd_partial_kernel");
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((unsigned)C), dim3(64), 0, st, part, chunks(M, C), M, C, gamma,
+    int64_t nch;
+    if (dA) {
+        nch = chunks(M, C);
+        hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)nch),
+                           dim3(256), 0, st, Y, M, C, ld, mean, invstd, gamma, beta, dA, ldd, dOut, ldo, arg, K,
+                           relu, chunk_rows(M, C), part);
+        PN2_LAUNCH_CHECK("bn_bwd_partial_kernel");
+    } else {  // scattered from the max: only the G argmax rows contribute
+        const int64_t G = M / K, gch = chunk_rows(G, C);
+        nch = (G + gch - 1) / gch;
+        PN2_REQUIRE(nch <= chunks(M, C), "pn2_bn_relu_backward_f32: gather partials exceed the workspace");
+        hipLaunchKernelGGL(bn_bwd_partial_gather_kernel, dim3((unsigned)((C + kTrCols - 1) / kTrCols), (unsigned)nch),
+                           dim3(256), 0, st, Y, G, C, ld, mean, invstd, gamma, beta, dOut, ldo, arg, K, relu, gch,
+                           part);
+        PN2_LAUNCH_CHECK("bn_bwd_partial_gather_kernel");
+    }
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((unsigned)C), dim3(64), 0, st, part, nch, M, C, gamma,
                        invstd, sxhat, dbeta, dgamma, dbias, sums);
     PN2_LAUNCH_CHECK("bn_bwd_final_kernel");
     hipLaunchKernelGGL(bn_bwd_apply_kernel,
