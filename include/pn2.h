@@ -32,6 +32,10 @@
  *                                                            (under autograd: train_rotation.py:99-133)
  *                          and the v1 shared MLPs' Conv1d + BatchNorm1d (+ ReLU) + max over N
  *                                                            model/pointnet_utils.py:31-35, 118-128
+ *   pn2_linear_rows_f32    eval Linear + BatchNorm1d (folded on the host) + ReLU of the FC tails
+ *                                                            model/pointnet_utils.py:33-40;
+ *                                                            pointnet_cls.py:26-28; rotation.py:45-49;
+ *                                                            pointnet2_cls_ssg.py:32-34
  *   pn2_prepare_points_f64 the scripts' input preparation: provider.normalization + torch.Tensor
  *                          + provider.splice_torch + transpose (+ the translation heads' mean)
  *                                                            provider.py:5-21, 166-180;
@@ -256,7 +260,7 @@ int pn2_bn_relu_backward_f32(const float *Y, int64_t M, int64_t C, int64_t ld, c
  * host): out[b*ldo + n] = act(sum_k x[b*ldx + k] * W[n*K + k] + bias[n]) for b < B (rows in
  * blocks of 16; each element computed the same way whatever B is),
  * W row-major [N][K], bias may be NULL; flags PN2_LINEAR_RELU applies the ReLU.  Float32 FMA.
- * Reference: pointnet_utils.py:36-40, pointnet_cls.py:18-27, rotation.py:45-49. ---- */
+ * Reference: pointnet_utils.py:33-40, pointnet_cls.py:26-28, rotation.py:45-49. ---- */
 #define PN2_LINEAR_RELU 1
 int pn2_linear_rows_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const float *W,
                         const float *bias, float *out, int64_t ldo, int64_t N, int flags,

@@ -2,7 +2,7 @@
 // 16.
 //
 // Reference: the FC tails of the PointNet-v1 networks, /root/reference/model/pointnet_utils.py:
-// 36-40 (T-Net fc1-fc3 + bn4/bn5), pointnet_cls.py:18-27 and the v1 heads' fc / bn_fc stacks
+// 36-40 (T-Net fc1-fc3 + bn4/bn5), pointnet_cls.py:26-28 and the v1 heads' fc / bn_fc stacks
 // (rotation.py:45-49), with each eval BatchNorm1d folded into W and bias on the host
 // (pn2/pointnet_utils.py linear_bn).  At a few rows these are matrix-vector products:
 // the weight (up to 1024 x 4096 floats) is read once, so the bound is HBM bytes of W -- and in

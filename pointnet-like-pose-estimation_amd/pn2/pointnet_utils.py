@@ -154,7 +154,7 @@ def _fold_linear(fc, bn, cache, extra=None):
 
 def linear_bn(x, fc, bn, cache, relu=True, extra=None):
     """Eval-mode ``relu(bn(fc(x)))`` (``bn`` may be None; ``extra`` a bias added after) as one
-    folded GEMM with the ReLU in its epilogue: the v1 FC tails (pointnet_utils.py:36-40, the
+    folded GEMM with the ReLU in its epilogue: the v1 FC tails (pointnet_utils.py:33-40, the
     heads' fc / bn_fc) on B rows are launch-bound, and BatchNorm1d's eval kernels cost more than
     the GEMM.  Device tensors run on pn2_linear_rows_f32 (the library GEMMs picked for these
     shapes take 5-13 us; CPU tensors, in tests, on F.linear).  Falls back to the modules when
