@@ -44,6 +44,7 @@ stream when ``run`` is called.
 """
 import atexit
 import ctypes
+import os
 
 import time
 
@@ -379,6 +380,19 @@ class GraphedPipeline(PipelinedForward):
         return (_sig((x,) + tuple(extra)), ops.current_precision()) + tuple(
             (t.data_ptr(), t._version) for t in ts)
 
+    def _split_index(self):
+        """The SA module after which a slot's compute graph ends and its tail graph begins.  The
+        last SA layer when it groups neighbourhoods; when it is a group_all layer (sa3 of every
+        reference head: M = B rows, a few hundred workgroups, latency-bound), the layer before
+        it, so the group_all layer runs with the head on the tail stream -- beside the next
+        batch's wide sa1/sa2 kernels instead of after them.  PN2_PIPE_SPLIT=last keeps the
+        old split (A/B)."""
+        k = len(self.sas) - 1
+        if (k > 0 and getattr(self.sas[k], "group_all", False) and
+                os.environ.get("PN2_PIPE_SPLIT", "") != "last"):
+            k -= 1
+        return k
+
     def _capture(self, x, extra, dev, draws):
         sl = _Slot()
         sl.x = x.clone()
@@ -411,7 +425,7 @@ class GraphedPipeline(PipelinedForward):
 
         cs = torch.cuda.Stream(dev)
         torch.cuda.synchronize(dev)
-        handle = self.sas[-1].register_forward_hook(split) if self.tail else None
+        handle = self.sas[self._split_index()].register_forward_hook(split) if self.tail else None
         try:
             with torch.no_grad(), torch.cuda.stream(cs):
                 with shard.start_source(static_start):
