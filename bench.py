@@ -67,8 +67,8 @@ DEFAULT_PRECISION = {"stress": "bf16"}
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)  # pipelined: K batches in one pass, fill amortised
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="ssg", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline sample")
