@@ -18,7 +18,7 @@ for s in $STEPS; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; ok $? smoke
       tail -5 $OUT/smoke.log ;;
     bench)
-      timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-20} --warmup 5 ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; ok $? bench
+      timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-100} --warmup 10 ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; ok $? bench
       tail -3 $OUT/bench.log ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-timer ${BENCH_ARGS:-} > $OUT/prof.log 2>&1; ok $? prof
