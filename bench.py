@@ -53,12 +53,16 @@ CONFIGS = {
     # name: (head, clouds per GPU, points, cloud kind, description)
     "ssg": ("pointnet2_cls_ssg", 32, 1024, "uniform3", "pointnet2_cls_ssg forward, B=32/GPU, N=1024"),
     "msg": ("pointnet2_cls_msg", 32, 4096, "uniform3", "pointnet2_cls_msg forward, B=32/GPU, N=4096"),
-    "pose": ("rotation_ssg+translation_ssg", 8, 2048, "onehot10",
-             "rotation_ssg + translation_ssg forward, B=8/GPU (64 on 8 GPUs), N=2048, 10-ch"),
+    # BASELINE config 4: B=64 batch-sharded across the GPUs (strong scaling: the global batch is
+    # fixed, each rank runs its shard_range slice)
+    "pose": ("rotation_ssg+translation_ssg", 64, 2048, "onehot10",
+             "rotation_ssg + translation_ssg forward, global B=64 sharded over the GPUs, N=2048, 10-ch"),
     "stress": ("pointnet2_cls_ssg", 128, 16384, "uniform3", "pointnet2_cls_ssg forward, B=128/GPU, N=16384"),
     # BASELINE config 1 (the reference runs it on the CPU): PointNet-v1 on the v1 kernels
     "v1": ("pointnet_cls", 8, 1024, "uniform3", "pointnet_cls (PointNet v1) forward, B=8/GPU, N=1024"),
 }
+# configs whose batch is a fixed global batch split over the ranks; the others are B per GPU
+STRONG = {"pose"}
 # MLP arithmetic per config: BASELINE config 5 (stress) asks for features/MLP in bf16, the
 # others are the reference's fp32
 DEFAULT_PRECISION = {"stress": "bf16"}
@@ -91,7 +95,35 @@ def parse():
                     help="shared-MLP arithmetic (default: bf16 for --config stress, else fp32)")
     ap.add_argument("--geometry-cus", type=int, default=0,
                     help="CUs reserved for the FPS chain (0: streams share every CU)")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="no GPU work: ranks join a gloo group, all_gather their shard ranges "
+                         "and rank 0 prints a JSON line with n_gpus (tests the launcher on CPU)")
     return ap.parse_args()
+
+
+def plumbing_check(a):
+    """CPU check of the multi-rank plumbing: the process group, the shard split of the global
+    batch and the uneven-shard all_gather -- the launch path a --gpus N run takes, minus the
+    GPU."""
+    from pn2 import shard
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    _, B, N, _, desc = CONFIGS[a.config]
+    gB = B if a.config in STRONG else B * world
+    lo, hi = shard.shard_range(gB, rank, world)
+    rows = shard.all_gather_rows(torch.arange(lo, hi, dtype=torch.float64)[:, None])
+    ok = rows[:, 0].tolist() == list(range(gB))
+    if rank == 0:
+        print(json.dumps({"plumbing_check": ok, "n_gpus": world, "global_batch": gB,
+                          "rank_env": {k: os.environ.get(k) for k in
+                                       ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")},
+                          "config": {"workload": desc, "parallelism": "dp%d" % world}}))
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
 
 
 def build_models(cfg, dev):
@@ -109,14 +141,17 @@ def build_models(cfg, dev):
     return names, models
 
 
-def make_inputs(cfg, B, lo, dev, rank):
+def make_inputs(cfg, B, lo, dev, rank, gB):
     import cases
     head, _, N, kind, _ = CONFIGS[cfg]
-    # per-rank shard of a seeded global batch (large configs: per-rank seed, same distribution)
-    x = cases.cloud(kind, B, N, 7 + rank)
+    if cfg in STRONG:  # this rank's slice [lo, lo + B) of one seeded global batch
+        x = cases.cloud(kind, gB, N, 7)[lo:lo + B]
+        mean = torch.randn(gB, 3, generator=torch.Generator().manual_seed(99))[lo:lo + B]
+    else:  # B clouds per rank: a per-rank seed, same distribution
+        x = cases.cloud(kind, B, N, 7 + rank)
+        mean = torch.randn(B, 3, generator=torch.Generator().manual_seed(99 + rank))
     x = x.permute(0, 2, 1).contiguous().to(dev)  # [B, C, N] model input
-    mean = torch.randn(B, 3, generator=torch.Generator().manual_seed(99 + rank)).to(dev)
-    return x, mean
+    return x, mean.to(dev)
 
 
 def step(names, models, x, mean, gB, lo):
@@ -145,7 +180,7 @@ def cpu_baseline(seconds):
     m = heads.ClsSSG()
     cases.randomize_bn(m, 2000)
     sd = {k: v.detach().float() for k, v in m.state_dict().items()}
-    Bs, N = 8, 1024
+    Bs, N = 32, 1024  # the metric's configuration (SSG B=32 N=1024)
     x = cases.cloud("uniform3", Bs, N, 7).permute(0, 2, 1).contiguous()
     with torch.no_grad():
         torch_ref.cls_ssg_forward(sd, x)  # warm-up
@@ -180,8 +215,72 @@ def load_traffic(cfg, op="pn2_sa_mlp_max_f32"):
         return None
 
 
+def rank_envs(n, port, base=None):
+    """The environment of each of n single-GPU ranks on this node (what torchrun sets)."""
+    envs = []
+    for r in range(n):
+        e = dict(os.environ if base is None else base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                  "LOCAL_WORLD_SIZE": str(n), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": str(port), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+        envs.append(e)
+    return envs
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, cmd=None, timeout=None):
+    """`bench.py --gpus N` without a launcher: start N child processes, one per GPU, each with
+    the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), then wait.  The parent
+    never touches the GPU (it only counts devices); rank 0 prints the JSON line on the shared
+    stdout.  If a rank fails the others are stopped and its exit code is returned."""
+    import subprocess
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)]
+    procs = [subprocess.Popen(cmd + list(argv), env=e) for e in rank_envs(n, free_port())]
+    rc, t0 = 0, time.time()
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r if r > 0 else 128 - r
+                    for q in live:
+                        q.terminate()
+            if timeout is not None and time.time() - t0 > timeout and live:
+                for q in live:
+                    q.kill()
+                rc = rc or 124
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     a = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        ndev = torch.cuda.device_count()  # counts devices without initialising one
+        if ndev < a.gpus and not a.plumbing_check:
+            sys.exit("bench.py: --gpus %d but only %d device(s) visible" % (a.gpus, ndev))
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != a.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s (the launcher started %s ranks)"
+                 % (a.gpus, env_world, env_world))
+    if a.plumbing_check:
+        return plumbing_check(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -197,7 +296,7 @@ def main():
     prec = a.precision or DEFAULT_PRECISION.get(a.config, "fp32")
     ctx = pn2.mlp_precision(prec)
     ctx.__enter__()  # for the whole run (the pipeline captures its graphs under it)
-    gB = B * world
+    gB = B if a.config in STRONG else B * world
     lo, hi = shard.shard_range(gB, rank, world)
     names, eager_models = build_models(a.config, dev)
     from pn2.graphs import GraphedForward
@@ -207,7 +306,7 @@ def main():
     if not has_sa and not a.no_pipeline:
         a.graph = True  # v1: no FPS chain to overlap; whole-forward HIP-graph replay instead
     models = [GraphedForward(m) for m in eager_models] if a.graph else eager_models
-    x, mean = make_inputs(a.config, hi - lo, lo, dev, rank)
+    x, mean = make_inputs(a.config, hi - lo, lo, dev, rank, gB)
     torch.manual_seed(1234)  # identical CPU RNG stream on every rank (FPS start draws)
 
     # single-head configs run software-pipelined (pn2.pipeline: the FPS chain of step i+1 on
@@ -313,7 +412,8 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "point-clouds/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True,
+            "scaling": "strong" if a.config in STRONG else "weak", "vs_baseline": None,
             "dtype": ("bf16 (MLP operands bf16, fp32 accumulate / BN / max; FPS/ball query f32)"
                       if prec == "bf16" else
                       "f32 (MLP products as 6-term split bf16, fp32 accumulate; FPS/ball query f32)"),

@@ -41,7 +41,12 @@ __device__ __forceinline__ unsigned row_max_u32(unsigned v) {
 #ifndef PN2_FPS_PRIO
 #define PN2_FPS_PRIO 3
 #endif
-template <int NT, int PPT, int CM, bool FIXED, bool LDSC>
+//
+// CR: channels held in registers (CR = CM normally).  Large clouds whose points do not fit the
+// register file with every channel keep only xyz (CR = 3) or nothing (CR = 0) there and re-read
+// the other channels of their points from the input each iteration (slow, but any N up to
+// NT*PPT); a cloud whose extra channels are constant (the one-hot class) never reads them.
+template <int NT, int PPT, int CM, bool FIXED, bool LDSC, int CR = CM>
 __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, int N, int Crt,
                                                  int64_t sb, int64_t sn, int64_t sc, int kind,
                                                  const int64_t *__restrict__ start, int S,
@@ -76,8 +81,18 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
     // end own padding points: coordinates 0, distance 0 -- they never beat a real point (real
     // points precede them and ties go to the first index).
     constexpr int PH = (PPT + 1) / 2;
-    pn2_f2 q[PH][CM];
+    static_assert(CR == CM || (CR <= 3 && !LDSC), "partial register residency: xyz or nothing");
+    constexpr int CQ = CR > 0 ? CR : 1;
+    pn2_f2 q[PH][CQ];
     unsigned dist[PPT];
+    // channel k of owned point j: registers, or the input (through `base`, which the serial
+    // loop launders every iteration so the compiler cannot hoist the re-reads out of it into
+    // registers the kernel does not have)
+    auto coord = [&](const float *base, int j, int k) -> float {
+        if (k < CR) return q[j >> 1][k < CQ ? k : 0][j & 1];
+        const int n = tid * PPT + j;
+        return (j < PPT && n < N && k < C) ? base[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
+    };
     int rule[PH];  // a pair shares its rule: the strided tail starts at an even index
 #pragma unroll
     for (int j = 0; j < 2 * PH; ++j) {
@@ -87,7 +102,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
 #pragma unroll
         for (int k = 0; k < CM; ++k) {
             pj[k] = (valid && k < C) ? P[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
-            q[j >> 1][k][j & 1] = pj[k];
+            if (k < CR) q[j >> 1][k < CQ ? k : 0][j & 1] = pj[k];
         }
         if (j < PPT) dist[j] = valid ? __float_as_uint(1e10f) : 0u;
         if ((j & 1) == 0) rule[j >> 1] = point_rule(kind, n, N);
@@ -124,7 +139,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
             cst = cst && __builtin_isfinite(v0);
 #pragma unroll
             for (int j = 0; j < 2 * PH; ++j)
-                if (j < PPT && tid * PPT + j < N) cst = cst && (q[j >> 1][k][j & 1] == v0);
+                if (j < PPT && tid * PPT + j < N) cst = cst && (coord(P, j, k) == v0);
         }
     }
     // block AND through a spare LDS word behind the key words (no static LDS: the cloud copy
@@ -149,6 +164,8 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
     for (int i = 0;; ++i) {
         if (tid == 0) sidx[i] = far;
         if (i == S - 1) break;
+        const float *Pl = P;
+        if constexpr (CR < CM) asm volatile("" : "+s"(Pl));
 
         // distances (two points per packed op) and the running min -- branchless
 #pragma unroll
@@ -158,7 +175,9 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
                 pn2_f2 s3[3];
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    const pn2_f2 d = q[h][k] - c[k];
+                    const pn2_f2 qk = k < CR ? q[h][k < CQ ? k : 0]
+                                             : pn2_f2{coord(Pl, 2 * h, k), coord(Pl, 2 * h + 1, k)};
+                    const pn2_f2 d = qk - c[k];
                     s3[k] = d * d;
                 }
                 dd = (s3[0] + s3[1]) + s3[2];
@@ -166,7 +185,9 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
                 pn2_f2 sq[CM];
 #pragma unroll
                 for (int k = 0; k < CM; ++k) {
-                    const pn2_f2 d = q[h][k] - c[k];
+                    const pn2_f2 qk = k < CR ? q[h][k < CQ ? k : 0]
+                                             : pn2_f2{coord(Pl, 2 * h, k), coord(Pl, 2 * h + 1, k)};
+                    const pn2_f2 d = qk - c[k];
                     sq[k] = d * d;
                 }
                 if constexpr (FIXED && CM == 3) dd = seq_sum<CM>(sq, C);  // every rule agrees for C=3
@@ -206,10 +227,17 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
             float bc[CM];
 #pragma unroll
             for (int k = 0; k < CM; ++k) {
-                float v = q[0][k].x;
+                if (k < CR) {
+                    float v = q[0][k < CQ ? k : 0].x;
 #pragma unroll
-                for (int j = 1; j < PPT; ++j) v = (bj == j) ? q[j >> 1][k][j & 1] : v;
-                bc[k] = v;
+                    for (int j = 1; j < PPT; ++j) v = (bj == j) ? q[j >> 1][k < CQ ? k : 0][j & 1] : v;
+                    bc[k] = v;
+                } else if (k < 3 || !xyz_only) {  // the owner lane reads its point's other channels
+                    const int n = tid * PPT + bj;
+                    bc[k] = (lane == ol && n < N && k < C) ? Pl[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
+                } else {
+                    bc[k] = 0.f;  // a constant channel: its difference is +0 whatever c[k] is
+                }
             }
             if constexpr (NW == 1) {
                 far = ol * PPT + __builtin_amdgcn_readlane(bj, ol);
@@ -310,7 +338,7 @@ using namespace pn2;
 
 extern "C" int64_t pn2_packed_stride(int64_t C) { return ((C + 1 + 3) / 4) * 4; }
 
-template <int NT, int PPT, int CM, bool FIXED>
+template <int NT, int PPT, int CM, bool FIXED, int CR = CM>
 static int launch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
                       int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx,
                       float *out_pts, float *out_packed, float *pts_packed, hipStream_t st) {
@@ -319,9 +347,13 @@ static int launch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t
     constexpr int SLOT = (CM + 2 + 3) & ~3;
     const size_t head = (size_t)((S + 3) & ~3) * 4 + 32;
     const size_t cloud = (size_t)N * (CM == 3 ? 4 : CM) * 4;
-    const bool ldsc = cloud <= (size_t)kFpsLdsCloud && head + cloud <= (size_t)160 * 1024;
+    const bool ldsc = CR == CM && cloud <= (size_t)kFpsLdsCloud && head + cloud <= (size_t)160 * 1024;
     const size_t lds = head + (ldsc ? cloud : (size_t)2 * NW * SLOT * 4);
-    if (ldsc) {
+    if constexpr (CR != CM) {
+        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, false, CR>), dim3((unsigned)B), dim3(NT), lds, st,
+                           pts, (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx, out_pts,
+                           out_packed, pts_packed, (int)pn2_packed_stride(C));
+    } else if (ldsc) {
         static const hipError_t attr = hipFuncSetAttribute(
             reinterpret_cast<const void *>(&fps_kernel<NT, PPT, CM, FIXED, true>),
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -363,9 +395,13 @@ static int dispatch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64
         if (N <= 8192) return launch_fps<1024, 8, CM, FIXED>(A);
     if constexpr (CAP >= 16384)
         if (N <= 16384) return launch_fps<1024, 16, CM, FIXED>(A);
+    // past the register-resident caps: xyz in registers, the other channels re-read from the
+    // input each iteration when they are not constant (the pose heads' one-hot clouds -- e.g.
+    // the 10000-point camera scans -- never read them)
+    if constexpr (CM > 3)
+        if (N <= 16384) return launch_fps<1024, 16, CM, FIXED, 3>(A);
 #undef A
-    return set_error(PN2_EUNSUPPORTED, "pn2_fps_f32: N=%lld exceeds the register-resident cap %d for C=%lld",
-                     (long long)N, CAP, (long long)C);
+    return set_error(PN2_EUNSUPPORTED, "pn2_fps_f32: N=%lld exceeds %d points", (long long)N, 16384);
 }
 
 extern "C" int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,

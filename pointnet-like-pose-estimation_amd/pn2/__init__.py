@@ -3,7 +3,7 @@ model/pointnet2_utils.py).  See DESIGN.md at the repository root."""
 from . import _lib, ops, shard  # noqa: F401  (ops loads libpn2.so and registers torch.ops.pn2.*)
 from .ops import mlp_precision  # noqa: F401
 from .pointnet2_utils import (  # noqa: F401
-    PointNetSetAbstraction, PointNetSetAbstractionMsg, farthest_point_sample, index_points,
+    eval_autograd, PointNetSetAbstraction, PointNetSetAbstractionMsg, farthest_point_sample, index_points,
     query_ball_point, sample_and_group, sample_and_group_all, square_distance)
 
 __version__ = "0.1.0"

@@ -1,7 +1,9 @@
 """Layer-config restatements of the reference's PointNet++ heads, built on pn2's SA modules.
 
 The reference heads import ``pointnet2_utils`` by bare name and run unchanged on the drop-in
-(see tests/test_gpu_reference_heads.py); the reference sources never travel to the GPU box, so
+(tests/test_host.py loads their checkpoints into these classes strictly and checks the
+constructor draws; tests/golden/make_goldens.py runs the reference heads themselves to make the
+head_*/full_* goldens the GPU tests compare against); the reference sources never travel to the GPU box, so
 the benchmark and the on-box parity tests build the same networks from these restatements.
 Submodules are created in the reference's order, so a ``torch.manual_seed`` before
 construction yields the identical parameters (pinned by a state_dict hash in the goldens) and
@@ -14,6 +16,7 @@ the ``state_dict`` keys match the reference's checkpoints.
   RotationMSG     /root/reference/model/rotation_msg.py:5-38
   TranslationMSG  /root/reference/model/translation_msg.py:5-44
   SignSSG         /root/reference/model/sign_ssg.py:5-36 (with the missing `import torch`)
+  SignMSG         /root/reference/model/sign_msg.py:5-36 (likewise)
 """
 import torch
 import torch.nn as nn
@@ -177,6 +180,22 @@ class SignSSG(_FCHead):
         return x, torch.sign(x - 0.5)
 
 
+class SignMSG(_FCHead):
+    def __init__(self, num_category=7):
+        super().__init__()
+        ch = 3 + num_category
+        self.sa1 = SAMsg(512, [16, 32, 64], [0.1, 0.2, 0.4], 0, [[32, 64, 128], [64, 128, 256], [96, 128, 256]], num_category=num_category)
+        self.sa2 = SA(None, None, None, 640 + ch, [256, 512, 1024], True)
+        self._make_fc(1)
+
+    def forward(self, points):
+        B = points.shape[0]
+        l1p, l1f = self.sa1(points, None)
+        _, l2f = self.sa2(l1p, l1f)
+        x = torch.sigmoid(self._fc(l2f.reshape(B, 1024)))
+        return x, torch.sign(x - 0.5)
+
+
 HEADS = {
     "pointnet2_cls_ssg": ClsSSG,
     "pointnet2_cls_msg": ClsMSG,
@@ -185,4 +204,5 @@ HEADS = {
     "rotation_msg": RotationMSG,
     "translation_msg": TranslationMSG,
     "sign_ssg": SignSSG,
+    "sign_msg": SignMSG,
 }

@@ -18,8 +18,9 @@ MI355X maps mask bits to XCDs).  Measured, SSG B=32 N=1024, graphed: shared 69.5
 clouds/s; 8 dedicated CUs (1 per XCD) 65.0k / 65.1k; 24 CUs 63.3k / 64.4k -- FPS co-resident
 with the MFMA kernels costs the chains less than the CUs a partition withholds from them.
 
-The tail of each forward -- everything after the last SA layer returns (the FC head, `post`) --
-can run on a third stream: it is a dozen tiny launches (the head's largest GEMM has 2
+The tail of each forward -- everything after the last SA layer returns (the FC head, `post`;
+in ``GraphedPipeline`` also a trailing group_all layer, see ``_split_index``) -- can run on a
+third stream: it is a dozen tiny launches (the head's largest GEMM has 2
 workgroups) that would otherwise sit on the compute stream between batch i's last MLP and batch
 i+1's first.  The switch is a forward hook on the last SA module, active only inside ``run``.
 The last SA layer's outputs are handed over with ``record_stream``; any other compute-stream
@@ -330,10 +331,13 @@ class GraphedPipeline(PipelinedForward):
       sa    the forward up to the last SA layer, replayed on the compute stream;
       head  the rest of the forward, replayed on a third stream with the geometry CUs (``tail``;
             with tail=False, head is part of sa).
-    The capture is split at the last SA layer by a forward hook (capture_end / capture_begin).
-    Events order the slot reuse: batch i+nslots's fps waits for batch i's sa (it overwrites the
-    slot's inputs and geometry outputs), batch i+nslots's sa waits for batch i's head (they share
-    a memory pool).  With 3 slots (default) the geometry chain has two batches of slack: at SSG
+    The capture is split by a forward hook (capture_end / capture_begin) after the last SA layer
+    that groups neighbourhoods (``_split_index``: a trailing group_all layer goes with the head;
+    the eager ``PipelinedForward`` tail still splits after the last SA layer).
+    Events order the slot reuse: batch i+nslots's fps waits until batch i's sa and head graphs
+    and the output clone have run (it overwrites the slot's inputs and geometry outputs, which
+    a group_all layer in the head graph still reads), batch i+nslots's sa waits for batch i's
+    head (they share a memory pool).  With 3 slots (default) the geometry chain has two batches of slack: at SSG
     its ~340 us (under MLP contention) is as long as the compute stream's work, so with 2 slots
     any jitter on either stream stalls the other.  Static memory makes the tail safe for every head here, including the translation
     heads' ``mean`` (see PipelinedForward).
@@ -385,10 +389,15 @@ class GraphedPipeline(PipelinedForward):
         last SA layer when it groups neighbourhoods; when it is a group_all layer (sa3 of every
         reference head: M = B rows, a few hundred workgroups, latency-bound), the layer before
         it, so the group_all layer runs with the head on the tail stream -- beside the next
-        batch's wide sa1/sa2 kernels instead of after them.  PN2_PIPE_SPLIT=last keeps the
-        old split (A/B)."""
+        batch's wide sa1/sa2 kernels instead of after them.  Only with shared CUs: with
+        geometry_cus > 0 the tail stream is masked to the geometry CUs, where a group_all MLP
+        would compete with FPS on a few CUs.  PN2_PIPE_SPLIT=last keeps the old split (A/B).
+
+        The head graph then reads the split layer's outputs -- sa2's centroids are a static
+        output of the slot's fps graph -- so the slot's next fps replay waits for the head
+        (``ev_read`` in ``run``), not only for the sa graph."""
         k = len(self.sas) - 1
-        if (k > 0 and getattr(self.sas[k], "group_all", False) and
+        if (k > 0 and getattr(self.sas[k], "group_all", False) and self.geometry_cus <= 0 and
                 os.environ.get("PN2_PIPE_SPLIT", "") != "last"):
             k -= 1
         return k
@@ -477,6 +486,7 @@ class GraphedPipeline(PipelinedForward):
             st.wait_stream(caller)
         ns = self.nslots
         ev_fps, ev_sa, ev_head = [None] * ns, [None] * ns, [None] * ns
+        ev_read = [None] * ns  # last read of a slot's fps outputs (sa, or head + clone)
         starts = self._draw_all(len(batches) - first)
 
         tr = self.trace  # optional list of per-batch timing events (tools/debug/gpipe_events.py)
@@ -494,8 +504,11 @@ class GraphedPipeline(PipelinedForward):
             sl = self._slots[s]
             geo = geos[j % len(geos)]
             with torch.cuda.stream(geo):
-                if ev_sa[s] is not None:  # batch j-ns is done with the slot's inputs
-                    geo.wait_event(ev_sa[s])
+                # batch j-ns is done with the slot's inputs and geometry outputs: its sa graph
+                # read them, and so did its head graph when the split put a group_all layer
+                # there (sa3 reads sa2's centroids, a static output of the fps graph)
+                if ev_read[s] is not None:
+                    geo.wait_event(ev_read[s])
                 mark(j, "geo0", geo)
                 sl.x.copy_(batches[j], non_blocking=True)
                 sl.start_buf.copy_(self._draw_row(starts, j - first), non_blocking=True)
@@ -529,6 +542,9 @@ class GraphedPipeline(PipelinedForward):
                         mark(i, "hd0", ts)
                         sl.head.replay()
                     out = _clone(sl.out)
+                    # recorded before `post` (e.g. an all_gather) so the next fps replay of
+                    # this slot does not wait for the collective
+                    ev_read[s] = ts.record_event()
                     if post is not None:
                         out = post(i, out)
                     ev_head[s] = ts.record_event()

@@ -75,16 +75,49 @@ def shard_range(global_batch, rank, world):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def all_gather_rows(local, group=None):
-    """Concatenate every rank's [b_r, ...] tensor along dim 0 (equal b_r; RCCL all_gather on
-    GPU tensors, gloo on CPU ones)."""
+def shard_sizes(global_batch, world):
+    """Clouds owned by every rank, in rank order (``shard_range``'s split)."""
+    return [hi - lo for lo, hi in (shard_range(global_batch, r, world) for r in range(world))]
+
+
+def all_gather_rows(local, group=None, sizes=None):
+    """Concatenate every rank's [b_r, ...] tensor along dim 0, in rank order (RCCL all_gather on
+    GPU tensors, gloo on CPU ones).
+
+    Shards may be uneven (``shard_range`` gives the remainder to the first ranks).  The row
+    counts come from `sizes`, else from the enclosing ``batch_shard`` (global batch -> every
+    rank's ``shard_range``), else from one extra all_gather of the counts.  Every rank's rows are
+    padded to the largest shard for the one fixed-size collective and trimmed after it."""
     if not dist.is_available() or not dist.is_initialized():
         return local
     world = dist.get_world_size(group)
     if world == 1:
         return local
     local = local.contiguous()
-    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
-                      device=local.device)
+    if sizes is None:
+        spec = getattr(_state, "spec", None)
+        if spec is not None and group is None:
+            sizes = shard_sizes(spec[0], world)
+            if sizes[dist.get_rank()] != local.shape[0]:
+                raise ValueError("all_gather_rows: %d rows on rank %d, batch_shard(%d) gives %d"
+                                 % (local.shape[0], dist.get_rank(), spec[0],
+                                    sizes[dist.get_rank()]))
+    if sizes is None:
+        n = torch.tensor([local.shape[0]], dtype=torch.long, device=local.device)
+        ns = torch.empty(world, dtype=torch.long, device=local.device)
+        dist.all_gather_into_tensor(ns, n, group=group)
+        sizes = [int(v) for v in ns.tolist()]
+    sizes = [int(v) for v in sizes]
+    if len(sizes) != world:
+        raise ValueError("all_gather_rows: %d sizes for %d ranks" % (len(sizes), world))
+    rest = tuple(local.shape[1:])
+    m = max(sizes)
+    if m != local.shape[0]:
+        pad = local.new_zeros((m,) + rest)
+        pad[:local.shape[0]] = local
+        local = pad
+    out = torch.empty((world * m,) + rest, dtype=local.dtype, device=local.device)
     dist.all_gather_into_tensor(out, local, group=group)
-    return out
+    if all(n == m for n in sizes):
+        return out
+    return torch.cat([out[r * m:r * m + n] for r, n in enumerate(sizes)])

@@ -91,6 +91,9 @@ INDEX_CASES = {
     'tiny':         ('uniform3', 1, 10, 'contig', 4, [(0.5, 2), (2.0, 10)], 19),
     'pose2048':     ('onehot10', 2, 2048, 'strided', 512, [(0.2, 32)], 20),
     'stress16k':    ('uniform3', 1, 16384, 'strided', 512, [(0.2, 32)], 21),
+    # the reference's real scans (points stored in the fixture): clustered, non-uniform density
+    'camera_strided': ('camera', 2, 10000, 'strided', 512, [(0.2, 32), (0.1, 16), (0.4, 128)], 22),
+    'camera10_contig': ('camera10', 2, 10000, 'contig', 512, [(0.2, 32), (0.4, 64)], 23),
 }
 
 # head-level cases: name -> (head, B, N, cloud kind, weight seed, forward seed)
@@ -101,6 +104,33 @@ HEAD_CASES = {
     'translation_ssg': ('translation_ssg', 2, 1024, 'onehot10', 103, 203),
     'rotation_msg': ('rotation_msg', 2, 1024, 'onehot10', 104, 204),
 }
+
+# head cases at the BASELINE shapes, the heads without a small case, and the reference's two
+# real scans: name -> (head, B, N, cloud kind, weight seed, forward seed, keep).  keep: the
+# clouds whose sa1 / sa2 features are stored (None: all) -- centroids of every layer, the last
+# SA feature and the head outputs are stored for the whole batch.  Synthetic inputs are
+# regenerated from the seed (the fixture holds their SHA-256); kind 'camera' / 'camera10' clouds
+# are /root/reference/camera_test/{bed,night_stand}.txt (np.loadtxt, xyz columns, the reference's
+# provider.normalization; 'camera10' + a one-hot label), stored in the fixture.
+HEAD_FULL_CASES = {
+    'cls_ssg_b32': ('pointnet2_cls_ssg', 32, 1024, 'uniform3', 110, 210, (0, 31)),
+    'cls_msg_n4096': ('pointnet2_cls_msg', 8, 4096, 'uniform3', 111, 211, (5,)),
+    'rotation_ssg_n2048': ('rotation_ssg', 8, 2048, 'onehot10', 112, 212, (0, 6)),
+    'translation_ssg_n2048': ('translation_ssg', 8, 2048, 'onehot10', 113, 213, (3, 7)),
+    'cls_ssg_n16384': ('pointnet2_cls_ssg', 2, 16384, 'uniform3', 114, 214, None),
+    'translation_msg': ('translation_msg', 2, 1024, 'onehot10', 115, 215, (1,)),
+    'sign_ssg': ('sign_ssg', 2, 1024, 'onehot10', 116, 216, None),
+    'sign_msg': ('sign_msg', 2, 1024, 'onehot10', 117, 217, (0,)),
+    'camera_cls_ssg': ('pointnet2_cls_ssg', 2, 10000, 'camera', 118, 218, None),
+    'camera_rotation_ssg': ('rotation_ssg', 2, 10000, 'camera10', 119, 219, None),
+}
+CAMERA_FILES = ('bed.txt', 'night_stand.txt')
+CAMERA_LABELS = (1, 4)  # one-hot classes of the two scans in 'camera10'
+
+
+def tensor_hash(t):
+    return hashlib.sha256(np.ascontiguousarray(t.detach().cpu().numpy()).tobytes()).hexdigest()
+
 
 # PointNet-v1 cases (/root/reference/model/pointnet_utils.py and the v1
 # heads): name -> (head module, B, N, cloud kind, weight seed, get_model kwargs)
@@ -131,6 +161,34 @@ def raw_batch(kind, B, N, seed, C=3):
         for b in range(B):
             x[b, rng.random(N) < 0.6] = x[b, 0]
     return x
+
+
+# the dataset tree of data_utils/ModelDataLoader.py (classes in its order, ModelDataLoader.py:51)
+CATEGORIES = ['cube', 'cuboid', 'cylinder', 'h_structure', 'double_cube', 'double_cylinder',
+              'cube_cylinder']
+
+
+def write_dataset_tree(root, items, n_points=1300, seed=11):
+    """<root>/<cls>/<cls>_NNNN{,_rot,_tran}.txt for every class, written the way
+    data_build/Cube.py:90-94 writes them (np.savetxt '%6f', comma-separated).  Deterministic:
+    the same call writes the same bytes anywhere (ids >= 6002 are the test split)."""
+    import os
+    rng = np.random.default_rng(seed)
+    for cls in CATEGORIES:
+        os.makedirs(os.path.join(root, cls), exist_ok=True)
+        for i in items:
+            base = os.path.join(root, cls, "%s_%04d" % (cls, i))
+            np.savetxt(base + ".txt", rng.uniform(-0.2, 0.2, (n_points + i % 50, 3)) + 0.5,
+                       fmt="%6f", delimiter=",")
+            np.savetxt(base + "_tran.txt", rng.normal(0, 0.1, (1, 3)), fmt="%6f", delimiter=",")
+            np.savetxt(base + "_rot.txt", rng.uniform(-3, 3, (1, 3)), fmt="%6f", delimiter=",")
+
+
+# end-to-end case (f4 -> f2 -> head, test_translation.py:70-83): the tree of
+# write_dataset_tree(items), the test split's items `index` loaded with np.random.seed(np_seed)
+# (random_sample draws), prepared, and run through `head` (weight seed, forward seed)
+E2E_CASE = dict(items=(6002, 6003), index=tuple(c * 1999 + j for c in range(7) for j in (1, 0)),
+                np_seed=5, head='translation_ssg', wseed=120, fseed=220)
 
 
 # input-preparation cases (provider.normalization + splice_torch + the translation mean):

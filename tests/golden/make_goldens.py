@@ -12,7 +12,12 @@ Files:
   head_<case>.npz   per-SA-layer outputs and head outputs for cases.HEAD_CASES (eval mode,
                     seeded weights + BN statistics; the weights are regenerated from the seed
                     and pinned by a state_dict SHA-256)
+  full_<case>.npz   the same at the BASELINE shapes, for the heads without a small case and on
+                    the reference's two real scans (cases.HEAD_FULL_CASES; features of a few
+                    clouds per batch, centroids / last feature / outputs of all)
   v1_<case>.npz     PointNet-v1 heads (cases.V1_CASES): encoder / T-Net / head outputs
+  e2e.npz           dataset tree -> ModelDataLoader -> preparation -> translation_ssg
+                    (cases.E2E_CASE), the reference's whole test-script input path
   prep_<case>.npz   input preparation (cases.PREP_CASES) by provider.py's own functions
   train_<case>.npz  training-mode SA forward + backward (cases.TRAIN_CASES)
 (`make_goldens.py v1` regenerates only the v1 files, etc.)
@@ -40,9 +45,32 @@ def _ref():
     return importlib.import_module("pointnet2_utils"), importlib
 
 
+def _camera_cloud(kind, B, N):
+    """The reference's two real scans (camera_test/*.txt, rows 'x,y,z,nx,ny,nz'): np.loadtxt,
+    xyz columns, the reference's provider.normalization, float32; 'camera10' adds the one-hot
+    of cases.CAMERA_LABELS with the reference's splice_torch.  -> [B, N, C] contiguous."""
+    normalization, splice_torch = _provider_functions()
+    assert B == len(cases.CAMERA_FILES)
+    raw = np.stack([np.loadtxt(os.path.join(os.path.dirname(REF_MODEL), "camera_test", f),
+                               delimiter=",")[:N, :3] for f in cases.CAMERA_FILES])
+    assert raw.shape == (B, N, 3), raw.shape
+    pts = torch.Tensor(normalization(raw))
+    if kind == "camera10":
+        pts = splice_torch(pts, torch.tensor(cases.CAMERA_LABELS))
+    return pts.contiguous()
+
+
+def _cloud(kind, B, N, seed):
+    if kind.startswith("camera"):
+        return _camera_cloud(kind, B, N)
+    return cases.cloud(kind, B, N, seed)
+
+
 def gen_index(P):
     for name, (kind, B, N, layout, S, bqs, seed) in cases.INDEX_CASES.items():
-        pts = cases.as_layout(cases.cloud(kind, B, N, seed), layout)
+        if only_cases and name not in only_cases:
+            continue
+        pts = cases.as_layout(_cloud(kind, B, N, seed), layout)
         torch.manual_seed(seed + 1000)
         start = torch.randint(0, N, (B,), dtype=torch.long)
         torch.manual_seed(seed + 1000)
@@ -97,6 +125,93 @@ def gen_heads(importlib):
             rec[tag + "_feature"] = f
         np.savez_compressed(os.path.join(HERE, "head_%s.npz" % name), **rec)
         print("head", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
+
+
+def gen_full(importlib):
+    """cases.HEAD_FULL_CASES: the reference heads at the BASELINE shapes, the heads without a
+    small case (translation_msg, sign_ssg, sign_msg) and the two real scans.  Stored: every
+    layer's centroids and the last SA layer's feature for the whole batch, sa1/sa2 features of
+    the `keep` clouds, the head outputs; the input itself only for the scans (synthetic clouds
+    are regenerated from their seed and pinned by a SHA-256)."""
+    import types
+    for name, (head, B, N, kind, wseed, fseed, keep) in cases.HEAD_FULL_CASES.items():
+        if only_cases and name not in only_cases:
+            continue
+        mod = importlib.import_module(head)
+        if not hasattr(mod, "torch"):  # sign_*.py use torch without importing it (sign_ssg.py:1-3, 34)
+            mod.torch = torch
+        assert isinstance(mod, types.ModuleType)
+        model = cases.build_head(mod.get_model, wseed)
+        x = _cloud(kind, B, N, wseed + 7)               # [B,N,C]
+        xin = x.permute(0, 2, 1).contiguous()           # [B,C,N] model input
+        rec = {"state_hash": np.array(cases.state_hash(model)),
+               "input_hash": np.array(cases.tensor_hash(xin))}
+        if kind.startswith("camera"):
+            rec["input"] = xin.numpy()
+        acts = {}
+        tags = [t for t in ("sa1", "sa2", "sa3") if hasattr(model, t)]
+
+        def hook(tag):
+            def f(_m, _inp, out):
+                acts[tag] = (out[0].detach().contiguous().numpy(), out[1].detach().contiguous().numpy())
+            return f
+        for tag in tags:
+            getattr(model, tag).register_forward_hook(hook(tag))
+        args = [xin]
+        if head.startswith("translation"):
+            mean = torch.randn(B, 3, generator=torch.Generator().manual_seed(wseed + 9))
+            rec["mean"] = mean.numpy()
+            args.append(mean)
+        torch.manual_seed(fseed)
+        with torch.no_grad():
+            out = model(*args)
+        outs = out if isinstance(out, tuple) else (out,)
+        for i, o in enumerate(outs):
+            rec["out%d" % i] = o.detach().numpy()
+        kept = np.arange(B) if keep is None else np.array(keep)
+        rec["keep"] = kept
+        for tag, (p, f) in acts.items():
+            rec[tag + "_points"] = p
+            rec[tag + "_feature"] = f if tag == tags[-1] else f[kept]
+        np.savez_compressed(os.path.join(HERE, "full_%s.npz" % name), **rec)
+        print("full", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
+
+
+def gen_e2e(importlib):
+    """The test script's whole input path (test_translation.py:70-83) by the reference: its
+    ModelDataLoader over a synthetic dataset tree (cases.write_dataset_tree), a DataLoader
+    batch, the provider preparation, and the translation_ssg head -> e2e.npz (prepared input,
+    mean, targets, prediction)."""
+    import tempfile
+    from types import SimpleNamespace
+    e = cases.E2E_CASE
+    normalization, splice_torch = _provider_functions()
+    sys.path.insert(0, os.path.join(os.path.dirname(REF_MODEL), "data_utils"))
+    loader_mod = importlib.import_module("ModelDataLoader")
+    head = importlib.import_module(e["head"])
+    with tempfile.TemporaryDirectory() as root:
+        root = root + "/"
+        cases.write_dataset_tree(root, e["items"])
+        ds = loader_mod.ModelDataLoader(root=root, args=SimpleNamespace(num_category=7), split="test")
+        np.random.seed(e["np_seed"])
+        dl = torch.utils.data.DataLoader(torch.utils.data.Subset(ds, list(e["index"])),
+                                         batch_size=len(e["index"]))
+        points, label, rot, target, sign = next(iter(dl))
+    points = points.data.numpy()
+    mean = torch.Tensor(np.mean(points[:, :3, :], axis=1))
+    points[:, :, 0:3] = normalization(points[:, :, 0:3])
+    points = torch.Tensor(points)
+    points = splice_torch(points, label)
+    points = points.transpose(2, 1)
+    model = cases.build_head(head.get_model, e["wseed"])
+    torch.manual_seed(e["fseed"])
+    with torch.no_grad():
+        pred = model(points, mean)
+    rec = {"prepared": points.contiguous().numpy(), "mean": mean.numpy(), "label": label.numpy(),
+           "target": target.numpy(), "rot": rot.numpy(), "sign": sign.numpy(),
+           "pred": pred.numpy(), "state_hash": np.array(cases.state_hash(model))}
+    np.savez_compressed(os.path.join(HERE, "e2e.npz"), **rec)
+    print("e2e", {k: v.shape for k, v in rec.items()})
 
 
 def gen_v1(importlib):
@@ -282,14 +397,23 @@ def gen_train_v1(importlib):
         print("trainv1", name, n, "outputs, min gap %.1e" % min(gaps))
 
 
+only_cases = set()  # `make_goldens.py full cls_ssg_b32`: just these cases of the chosen kinds
+
+
 def main():
     torch.set_num_threads(8)
     P, importlib = _ref()
-    only = sys.argv[1:]
+    kinds = ("index", "heads", "full", "e2e", "v1", "prep", "train", "trainv1")
+    only = [a for a in sys.argv[1:] if a in kinds]
+    only_cases.update(a for a in sys.argv[1:] if a not in kinds)
     if not only or "index" in only:
         gen_index(P)
     if not only or "heads" in only:
         gen_heads(importlib)
+    if not only or "full" in only:
+        gen_full(importlib)
+    if not only or "e2e" in only:
+        gen_e2e(importlib)
     if not only or "v1" in only:
         gen_v1(importlib)
     if not only or "prep" in only:

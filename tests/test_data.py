@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 import torch
 
+import cases
 from pn2 import data
 
 REF = "/root/reference"
@@ -87,15 +88,7 @@ def test_load_many_threads(tmp_path):
 
 def _make_tree(root, items, n_points=1300):
     """A few test-split items per class (ids 6002.. are test), written like data_build."""
-    rng = np.random.default_rng(11)
-    for cls in data.ModelDataLoader.cat:
-        os.makedirs(os.path.join(root, cls), exist_ok=True)
-        for i in items:
-            base = os.path.join(root, cls, "%s_%04d" % (cls, i))
-            np.savetxt(base + ".txt", rng.uniform(-0.2, 0.2, (n_points + i % 50, 3)) + 0.5,
-                       fmt="%6f", delimiter=",")
-            np.savetxt(base + "_tran.txt", rng.normal(0, 0.1, (1, 3)), fmt="%6f", delimiter=",")
-            np.savetxt(base + "_rot.txt", rng.uniform(-3, 3, (1, 3)), fmt="%6f", delimiter=",")
+    cases.write_dataset_tree(root, items, n_points)
 
 
 def _ref_loader_module(monkeypatch):
@@ -137,3 +130,53 @@ def test_dataset_matches_reference(tmp_path, monkeypatch):
     for a, b in zip(gb, wb):
         assert a.dtype == b.dtype and a.shape == b.shape
         np.testing.assert_array_equal(a.numpy(), b.numpy())
+
+
+def _e2e_batch(tmp_path):
+    """The E2E case's DataLoader batch through pn2.data (libpn2io reader, thread pool)."""
+    e = cases.E2E_CASE
+    root = str(tmp_path) + "/"
+    cases.write_dataset_tree(root, e["items"])
+    ds = data.ModelDataLoader(root=root, args=SimpleNamespace(num_category=7), split="test")
+    np.random.seed(e["np_seed"])
+    return ds.load_batch(list(e["index"]), threads=4)
+
+
+def test_e2e_reader_and_oracle_preparation_match_reference(tmp_path):
+    """f4 -> f2 on the CPU: the reader's batch, prepared by the oracle restatement of the
+    scripts' steps, equals the reference's whole test-script input path (e2e.npz: the
+    reference's ModelDataLoader + DataLoader + provider functions), bit for bit."""
+    import oracle
+    from conftest import load_golden
+    g = load_golden("e2e.npz")
+    points, label, rot, target, sign = _e2e_batch(tmp_path)
+    np.testing.assert_array_equal(label.numpy(), g["label"])
+    for a, k in ((rot, "rot"), (target, "target"), (sign, "sign")):
+        np.testing.assert_array_equal(_bits(a.numpy()), _bits(g[k]))
+    prepared, mean = oracle.prepare_points(points.numpy(), label.numpy(), 7, with_mean=True)
+    np.testing.assert_array_equal(_bits(prepared.transpose(0, 2, 1)), _bits(g["prepared"]))
+    np.testing.assert_array_equal(_bits(mean), _bits(g["mean"]))
+
+
+@pytest.mark.gpu
+def test_e2e_reader_prepare_head_on_gpu(tmp_path):
+    """f4 -> f2 -> head on the GPU box: pn2.data reads the dataset tree, pn2.provider
+    prepare_batch prepares it on the device (bit-exact to the reference's prepared input), and
+    the translation_ssg head on the fused kernels reproduces the reference's prediction."""
+    from conftest import load_golden
+    from pn2 import heads as H
+    from pn2.provider import prepare_batch
+    e = cases.E2E_CASE
+    g = load_golden("e2e.npz")
+    points, label, rot, target, sign = _e2e_batch(tmp_path)
+    x, mean = prepare_batch(points, label, with_mean=True)
+    np.testing.assert_array_equal(_bits(x.cpu().numpy()), _bits(g["prepared"]))
+    np.testing.assert_array_equal(_bits(mean.cpu().numpy()), _bits(g["mean"]))
+    model = cases.build_head(H.HEADS[e["head"]], e["wseed"])
+    assert cases.state_hash(model) == str(g["state_hash"])
+    model = model.to("cuda").eval()
+    torch.manual_seed(e["fseed"])
+    with torch.no_grad():
+        pred = model(x, mean)
+    want = g["pred"]
+    np.testing.assert_allclose(pred.cpu().numpy(), want, rtol=1e-4, atol=1e-4 * np.abs(want).max())

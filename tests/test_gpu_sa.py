@@ -121,26 +121,6 @@ def test_ssg_baseline_config_full_size():
     np.testing.assert_array_equal(o1[0].cpu().numpy(), o2[0].cpu().numpy())
 
 
-def test_msg_baseline_config_full_size():
-    """BASELINE config 3 (pointnet2_cls_msg, B=32, N=4096): shapes, determinism, and the
-    autograd (torch) path agreeing with the fused path within tolerance."""
-    from pn2 import heads as H
-    torch.manual_seed(1)
-    model = H.ClsMSG().eval()
-    cases.randomize_bn(model, 2)
-    model = model.to(DEV)
-    B, N = 32, 4096
-    x = cases.cloud("uniform3", B, N, 43).permute(0, 2, 1).contiguous().to(DEV)
-    torch.manual_seed(3)
-    with torch.no_grad():
-        p1, f1 = model.sa1(x, None)
-    torch.manual_seed(3)
-    p2, f2 = model.sa1._forward_autograd(x, None)
-    np.testing.assert_array_equal(p1.cpu().numpy(), p2.detach().cpu().numpy())
-    assert f1.shape == (B, 320, 512)
-    assert_feat_close(f1.cpu().numpy(), f2.detach().cpu().numpy())
-
-
 def test_pose_heads_sharded_equals_unsharded():
     """BASELINE config 4 semantics on one GPU: rotation_ssg + translation_ssg B=64 N=2048
     one-hot; running the batch as 8 shards (with the full-batch FPS draws sliced) reproduces
@@ -417,3 +397,67 @@ def test_graphed_pipeline_multihead_matches_eager(layout):
         for k, (a, b) in enumerate(zip(g, w)):
             np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * float(np.abs(b).max()),
                                        err_msg="head %d of batch %d" % (k, i))
+
+
+def test_graphed_pipeline_delayed_tail_matches_eager():
+    """A slow tail stream must not let a slot's next fps replay overwrite geometry that the slot's
+    head graph still reads: with the group_all split, sa3 (in the head graph) reads sa2's
+    centroids, a static output of the fps graph.  `post` runs on the tail stream and sleeps
+    there, so every head replay starts late; the geometry streams run ahead as far as the
+    events allow.  The l3 features must still be the eager bits."""
+    from pn2 import heads as H
+    from pn2.pipeline import GraphedPipeline
+    torch.manual_seed(8)
+    model = H.ClsSSG().eval()
+    cases.randomize_bn(model, 8)
+    model = model.to(DEV)
+    B, N = 16, 1024
+    xs = [cases.cloud("uniform3", B, N, 200 + i).permute(0, 2, 1).contiguous().to(DEV)
+          for i in range(9)]
+    torch.manual_seed(17)
+    with torch.no_grad():
+        want = [model(x)[1].cpu().numpy() for x in xs]
+
+    def slow(i, o):
+        torch.cuda._sleep(4_000_000)  # on the tail stream, before the next head replay
+        return o
+
+    gp = GraphedPipeline(model, tail=True)
+    assert gp._split_index() == 1  # sa3 (group_all) is in the head graph
+    torch.manual_seed(17)
+    got = [o[1].cpu().numpy() for o in gp.run(xs, post=slow)]
+    for i, (g, w) in enumerate(zip(got, want)):
+        np.testing.assert_array_equal(g, w, err_msg="l3f of batch %d" % i)
+
+
+def test_eval_without_no_grad_takes_fused_path():
+    """model.eval() without torch.no_grad() (mutilthreading/predict_test.py:44-63) runs the
+    fused split-bf16 kernels and gives the no_grad bits; a backward through those outputs raises
+    instead of silently leaving the SA weights without gradients; inside pn2.eval_autograd() the
+    same forward is the differentiable torch formulation (eval-mode fine-tuning)."""
+    import pn2
+    from pn2 import _lib
+    from pn2 import heads as H
+    torch.manual_seed(3)
+    model = H.ClsSSG().eval()
+    cases.randomize_bn(model, 3)
+    model = model.to(DEV)
+    x = cases.cloud("uniform3", 4, 1024, 5).permute(0, 2, 1).contiguous().to(DEV)
+    torch.manual_seed(1)
+    with torch.no_grad():
+        want = model(x)
+    torch.manual_seed(1)
+    got = model(x)  # autograd on, parameters require grad
+    assert _lib.load().pn2_sa_mlp_last_path() == _lib.PATH_SPLIT_BF16
+    np.testing.assert_array_equal(got[1].detach().cpu().numpy(), want[1].cpu().numpy())
+    np.testing.assert_allclose(got[0].detach().cpu().numpy(), want[0].cpu().numpy(),
+                               rtol=1e-5, atol=1e-6)
+    with pytest.raises(RuntimeError, match="fused inference kernels"):
+        got[0].sum().backward()
+    model.zero_grad()
+    torch.manual_seed(1)
+    with pn2.eval_autograd():
+        ft = model(x)
+    ft[0].sum().backward()
+    assert model.sa1.mlp_convs[0].weight.grad is not None
+    assert_feat_close(ft[1].detach().cpu().numpy(), want[1].cpu().numpy())

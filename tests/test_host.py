@@ -93,38 +93,54 @@ def test_sharded_draws_match_unsharded():
     assert shard.shard_range(10, 0, 4) == (0, 3) and shard.shard_range(10, 3, 4) == (8, 10)
 
 
-def _gloo_worker(rank, world, port, out):
+def _gloo_worker(rank, world, port, out, B=8):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sys.path.insert(0, PKG)
     from pn2 import shard
-    B = 8
     lo, hi = shard.shard_range(B, rank, world)
     torch.manual_seed(21)
     with shard.batch_shard(B, lo):
         starts = shard.draw_start(hi - lo, 100)
-    local = torch.stack([starts.double(), torch.full((hi - lo,), float(rank), dtype=torch.float64)], 1)
-    got = shard.all_gather_rows(local)
+        local = torch.stack([starts.double(), torch.full((hi - lo,), float(rank), dtype=torch.float64)], 1)
+        got_spec = shard.all_gather_rows(local)  # row counts from batch_shard
+    got = shard.all_gather_rows(local)  # row counts gathered from the ranks
+    got_sizes = shard.all_gather_rows(local, sizes=shard.shard_sizes(B, world))
     if rank == 0:
-        out.put(got.numpy())
+        out.put((got.numpy(), got_spec.numpy(), got_sizes.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_world2_all_gather_and_rng_parity():
+@pytest.mark.parametrize("B,world", [(8, 2), (7, 2), (7, 3)])
+def test_gloo_all_gather_and_rng_parity(B, world):
+    """world_size 2-3 over gloo: every rank draws the full batch's FPS starts and keeps its
+    shard; the gathered rows are the unsharded draw, in rank order -- also for uneven shards
+    (B % world != 0), whether the row counts come from batch_shard, an explicit list, or a
+    gather of the counts."""
     import random
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = random.randint(20000, 40000)
-    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, q, B)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    res = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     torch.manual_seed(21)
-    want = torch.randint(0, 100, (8,), dtype=torch.long).numpy()
-    np.testing.assert_array_equal(got[:, 0].astype(np.int64), want)
-    np.testing.assert_array_equal(got[:, 1], [0, 0, 0, 0, 1, 1, 1, 1])
+    want = torch.randint(0, 100, (B,), dtype=torch.long).numpy()
+    owner = np.concatenate([np.full(hi - lo, r) for r, (lo, hi) in
+                            enumerate(shard_ranges(B, world))])
+    for got in res:
+        assert got.shape == (B, 2)
+        np.testing.assert_array_equal(got[:, 0].astype(np.int64), want)
+        np.testing.assert_array_equal(got[:, 1], owner)
+
+
+def shard_ranges(B, world):
+    sys.path.insert(0, PKG)
+    from pn2 import shard
+    return [shard.shard_range(B, r, world) for r in range(world)]

@@ -81,12 +81,15 @@ def test_v1_heads_rebuild_reference_weights(name):
 
 @pytest.mark.parametrize("name", golden_names("v1_"))
 def test_v1_autograd_path_matches_goldens(name):
-    """Grad-enabled eval forward = the reference's torch formulation, on the CPU."""
+    """Eval forward inside pn2.eval_autograd() = the reference's torch formulation, on the
+    CPU."""
+    import pn2
     g = load_golden("v1_%s.npz" % name)
     model, _ = _build(name)
     acts = {}
     _hooks(model, acts)
-    out = model(*_args(g, "cpu"))
+    with pn2.eval_autograd():
+        out = model(*_args(g, "cpu"))
     _check(g, out, acts, 1e-6, 1e-6)
 
 
@@ -104,7 +107,8 @@ def test_v1_eval_on_cpu_raises():
 @pytest.mark.parametrize("head", ["pointnet_cls", "rotation", "pose"])
 def test_reference_v1_heads_import_drop_in_unchanged(head, monkeypatch):
     """The reference's own v1 head files, with `pointnet_utils` resolving to the drop-in, load
-    a reference-built state_dict strictly and run (autograd path) to the reference's numbers;
+    a reference-built state_dict strictly and run (pn2.eval_autograd: the torch path) to the
+    reference's numbers;
     eval without autograd reaches the kernels (CPU tensor -> loud error).  (translation / sign
     / width keep their whole conv stack in the head file: only pn2.heads_v1 accelerates them.)"""
     import importlib
@@ -125,7 +129,9 @@ def test_reference_v1_heads_import_drop_in_unchanged(head, monkeypatch):
     sys.modules.pop(head, None)
     model.eval()
     x = torch.rand(2, 3 if head in ("pointnet_cls", "pose") else 10, 64)
-    a, b = ref(x), model(x)
+    import pn2
+    with pn2.eval_autograd():
+        a, b = ref(x), model(x)
     for u, v in zip(a if isinstance(a, tuple) else (a,), b if isinstance(b, tuple) else (b,)):
         np.testing.assert_array_equal(u.detach().numpy(), v.detach().numpy())
     with pytest.raises(RuntimeError, match="ROCm device tensors only"):
