@@ -85,7 +85,7 @@ def parse():
                     help="eager pipeline: run the head on its own stream (default off there)")
     ap.add_argument("--no-tail", action="store_true",
                     help="graphed pipeline: keep the head on the compute stream")
-    ap.add_argument("--slots", type=int, default=3,
+    ap.add_argument("--slots", type=int, default=4,
                     help="graphed pipeline: batches in flight (geometry runs slots-1 ahead)")
     ap.add_argument("--geometry-streams", type=int, default=2,
                     help="graphed pipeline: 2 = consecutive batches' FPS chains on two streams")

@@ -55,7 +55,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 8
+#define PN2_ABI_VERSION 9
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -71,8 +71,9 @@ int64_t pn2_packed_stride(int64_t C);
  *   out_pts    [B,S,C] float32 contiguous, or NULL   index_points(points, fps_idx)
  *   out_packed [B,S,cp] float32, or NULL         packed centroids (contiguous-layout ssq)
  *   pts_packed [B,N,cp] float32, or NULL         packed input points (input-layout ssq)
- * The cloud is register-resident: N <= 16384 for C == 3, N <= 8192 for C == 10, N <= 4096 for
- * other C <= 16 (else PN2_EUNSUPPORTED); S <= 8192. */
+ * N <= 16384 and C <= 16 (else PN2_EUNSUPPORTED); S <= 8192.  The cloud is register-resident
+ * up to N = 16384 for C == 3, 8192 for C == 10, 4096 for other C; past that the channels after
+ * xyz are re-read from pts each iteration unless they are constant over the cloud (one-hot). */
 int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
                 int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
                 float *out_packed, float *pts_packed, void *stream);
@@ -88,6 +89,13 @@ int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64
 int pn2_ball_query_f32(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N,
                        int64_t S, int64_t C, double radius, int64_t K, int64_t *out_idx,
                        void *stream);
+/* The same, also writing out_cnt [B,S] int32 (or NULL): the number of distinct neighbours of
+ * each centroid, min(hits, K) -- out_idx entries past it repeat entry 0.  Passed to the SA MLP
+ * (pn2_sa_src.cnt) it lets the chain compute only those rows (the max over a group does not
+ * change without repeats). */
+int pn2_ball_query_cnt_f32(const float *pts_packed, const float *ctr_packed, int64_t B,
+                           int64_t N, int64_t S, int64_t C, double radius, int64_t K,
+                           int64_t *out_idx, int32_t *out_cnt, void *stream);
 
 /* square_distance(src, dst) -> out [B,S,N] float32 from packed records of src [B,S,cp] and
  * dst [B,N,cp] (same float32 recipe as the ball query). */
@@ -170,6 +178,9 @@ typedef struct pn2_sa_src {
     const int64_t *idx;                   /* [B,S,K] int64 contiguous (group modes)     */
     const float *rows; int64_t rs;        /* PN2_SRC_ROWS: [M][rs]                      */
     int64_t B, N, C, D, S, K;             /* rows M = B*S*K (GROUP_ALL: S=1, K=N)       */
+    const int32_t *cnt;                   /* [B,S] distinct neighbours per group
+                                             (pn2_ball_query_cnt_f32), or NULL: group
+                                             modes then compute only those rows          */
 } pn2_sa_src;
 
 /* Bytes of workspace pn2_sa_mlp_max_f32 needs for this layer chain: 0 when the chain runs as

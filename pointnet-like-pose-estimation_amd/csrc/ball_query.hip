@@ -19,7 +19,8 @@ __global__ __launch_bounds__(64 * WPB) void ball_query_kernel(const float *__res
                                                               const float *__restrict__ ctr,
                                                               int64_t B, int N, int S, int C,
                                                               float r2, int K, int small,
-                                                              int64_t *__restrict__ out) {
+                                                              int64_t *__restrict__ out,
+                                                              int *__restrict__ out_cnt) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t q = (int64_t)blockIdx.x * WPB + w;  // centroid (b*S + s)
@@ -75,6 +76,8 @@ __global__ __launch_bounds__(64 * WPB) void ball_query_kernel(const float *__res
         }
     }
     for (int k = cnt + lane; k < K; k += 64) o[k] = first;
+    // distinct neighbours: entries past them repeat entry 0 (the SA chain computes only these)
+    if (out_cnt && lane == 0) out_cnt[q] = min(cnt, K);
 }
 
 }  // namespace pn2
@@ -83,12 +86,12 @@ using namespace pn2;
 
 template <int CP>
 static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, int64_t S,
-                     int64_t C, float r2, int64_t K, int64_t *out, hipStream_t st) {
+                     int64_t C, float r2, int64_t K, int64_t *out, int *cnt, hipStream_t st) {
     constexpr int WPB = 4;
     const int64_t nq = B * S;
     hipLaunchKernelGGL((ball_query_kernel<CP, WPB>), dim3((unsigned)((nq + WPB - 1) / WPB)),
                        dim3(64 * WPB), 0, st, pp, cp_, B, (int)N, (int)S, (int)C, r2, (int)K,
-                       (int)(S * N * C < 400), out);
+                       (int)(S * N * C < 400), out, cnt);
     PN2_LAUNCH_CHECK("ball_query_kernel");
     return PN2_OK;
 }
@@ -96,6 +99,13 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
 extern "C" int pn2_ball_query_f32(const float *pts_packed, const float *ctr_packed, int64_t B,
                                   int64_t N, int64_t S, int64_t C, double radius, int64_t K,
                                   int64_t *out_idx, void *stream) {
+    return pn2_ball_query_cnt_f32(pts_packed, ctr_packed, B, N, S, C, radius, K, out_idx, nullptr,
+                                  stream);
+}
+
+extern "C" int pn2_ball_query_cnt_f32(const float *pts_packed, const float *ctr_packed, int64_t B,
+                                      int64_t N, int64_t S, int64_t C, double radius, int64_t K,
+                                      int64_t *out_idx, int32_t *out_cnt, void *stream) {
     PN2_REQUIRE(pts_packed && ctr_packed && out_idx, "pn2_ball_query_f32: null pointer");
     PN2_REQUIRE(B >= 0 && N >= 1 && S >= 0 && C >= 1 && C <= kMaxC && K >= 1,
                 "pn2_ball_query_f32: bad shape B=%lld N=%lld S=%lld C=%lld K=%lld", (long long)B,
@@ -107,11 +117,11 @@ extern "C" int pn2_ball_query_f32(const float *pts_packed, const float *ctr_pack
     const float r2 = (float)(radius * radius);
     hipStream_t st = as_stream(stream);
     const int64_t cp = pn2_packed_stride(C);
-    if (cp == 4) return launch_bq<4>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, st);
-    if (cp == 8) return launch_bq<8>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, st);
-    if (cp == 12) return launch_bq<12>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, st);
-    if (cp == 16) return launch_bq<16>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, st);
-    if (cp == 20) return launch_bq<20>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, st);
+    if (cp == 4) return launch_bq<4>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
+    if (cp == 8) return launch_bq<8>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
+    if (cp == 12) return launch_bq<12>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
+    if (cp == 16) return launch_bq<16>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
+    if (cp == 20) return launch_bq<20>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
     return set_error(PN2_EUNSUPPORTED, "pn2_ball_query_f32: C=%lld", (long long)C);
 }
 

@@ -66,7 +66,20 @@ struct ChainArgs {
     const float *w0x;
     int w0x_row;
     int lds_u, u_groups;
+    // compact neighbourhoods (pool_mode 3, given the ball query's distinct-neighbour counts): a
+    // group's rows past its distinct neighbours repeat its first neighbour
+    // (pointnet2_utils.py:87-89), and the max over the group is the same without them -- so
+    // only each group's distinct rows are computed, in 8-row units laid out in group order, 4
+    // per wave (compact_scan_kernel).  cdesc[wg].x = the workgroup's first group within its
+    // cloud (y < 0: an unused workgroup); cunits[wg*16 + i] = (group - first) << 8 | unit of
+    // the group << 4 | last unit of the group << 3 | (rows of the unit - 1), or -1 (unused).
+    const int *cunits;
+    const int2 *cdesc;
+    int wpc;  // workgroups per cloud
 };
+
+constexpr int kUnitRows = 8;
+constexpr int kUnitsPerWG = kChainRows / kUnitRows;  // 16
 
 template <int NP>
 __device__ __forceinline__ Split load_w(const ChainLayer &L, int t, int kb, int lane) {
@@ -142,10 +155,12 @@ __device__ __forceinline__ void ring_issue(const bf16x8 *frag, int64_t plane, ch
 }
 
 // step 2 above: this wave's copies of the kStages-2 younger stages (NP each) may stay in flight
-template <int NP>
+// (KS == 2, the compact launches' shallower ring: nothing younger is in flight)
+template <int NP, int KS>
 __device__ __forceinline__ void stage_wait() {
-    static_assert(kStages == 3, "stage_wait count");
-    if constexpr (NP == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    static_assert(KS == 2 || KS == 3, "stage_wait count");
+    if constexpr (KS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (NP == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
 }
 
@@ -163,7 +178,8 @@ __device__ __forceinline__ void stage_barrier() {
 // KB0M > 0: the layer-0 input (<= KB0M k-blocks) is gathered once into registers and layer 0 runs
 // tile by tile from the ring like layers 1 and 2; KB0M == 0: layer 0 streams its input blocks
 // (k-outer, every output tile accumulating) with ordinary loads and the ring starts at layer 1.
-template <int T0, int T1, int KB0M, int NP>
+// KS: weight-ring stages (3; 2 for compact launches, whose LDS group pool needs the room)
+template <int T0, int T1, int KB0M, int NP, int KS>
 __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_eu(3))) void sa_chain_kernel(
     const ChainArgs A) {
     constexpr int kStepBytes = step_bytes<NP>(), kStageBytes = stage_bytes<NP>();
@@ -178,7 +194,18 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     const pn2_sa_src &s = A.src;
     const ChainLayer &L0 = A.L[0], &L1 = A.L[1], &L2 = A.L[2];
     const int coutL = 32 * L2.tiles;
-    const int gpb = kChainRows / A.K;  // groups per workgroup (pool_mode 1)
+    const bool compact = A.pool_mode == 3;
+    unsigned c_g0 = 0;
+    int c_ng = 0, c_flags = 0;
+    if (compact) {
+        const int2 d = A.cdesc[blockIdx.x];
+        if (d.y < 0) return;  // no rows left for this workgroup (uniform: before any barrier)
+        c_g0 = (unsigned)(blockIdx.x / A.wpc) * (unsigned)A.S + (unsigned)d.x;
+        c_ng = d.y & 255;
+        c_flags = d.y >> 8;
+    }
+    // groups per workgroup of the LDS pool (pool_mode 1; compact: up to one per unit)
+    const int gpb = compact ? kUnitsPerWG : kChainRows / A.K;
 
     // stage BN scale/shift of the three layers: [al0|be0|al1|be1|al2|be2]
     float *bn = reinterpret_cast<float *>(csm + A.lds_bn);
@@ -187,9 +214,9 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     for (int e = tid; e < 32 * T0; e += 64 * kChainWaves) { al0[e] = L0.alpha[e]; be0[e] = L0.beta[e]; }
     for (int e = tid; e < 32 * T1; e += 64 * kChainWaves) { al1[e] = L1.alpha[e]; be1[e] = L1.beta[e]; }
     for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
-    if (A.pool_mode == 1)
+    if (A.pool_mode == 1 || compact)
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
-    const unsigned g0 = (unsigned)(blockIdx.x * kChainRows) / (unsigned)A.K;  // first group
+    const unsigned g0 = compact ? c_g0 : (unsigned)(blockIdx.x * kChainRows) / (unsigned)A.K;  // first group
     float *ulds = reinterpret_cast<float *>(csm + A.lds_u);
     if constexpr (KB0M < 0) {
         // u[g][c] = sum_k W0[c][xyz k] * centroid[g][k]: the centroid's share of layer 0, which
@@ -227,7 +254,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     const int n0 = T0 * L0.kb;
     auto issue_stage = [&](int st) {  // this wave's step of stage st
         const int x = st * kChainWaves + wave;
-        char *dst = ring + (st % kStages) * kStageBytes + wave * kStepBytes;
+        char *dst = ring + (st % KS) * kStageBytes + wave * kStepBytes;
         if constexpr (KB0M > 0) {
             if (x < n0) issue_l(L0, x % T0, x / T0, dst);
             else issue1(x - n0, dst);
@@ -240,22 +267,36 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         if ((nread & (kChainWaves - 1)) == 0) {  // first step of a stage
             const int st = nread / kChainWaves;
             ring_fence();
-            stage_wait<NP>();
+            stage_wait<NP, KS>();
             stage_barrier();
-            issue_stage(st + kStages - 1);
+            issue_stage(st + KS - 1);
         }
-        const Split w = ring_readN<NP>(ring + ((nread / kChainWaves) % kStages) * kStageBytes +
+        const Split w = ring_readN<NP>(ring + ((nread / kChainWaves) % KS) * kStageBytes +
                                       (nread & (kChainWaves - 1)) * kStepBytes, lane);
         ++nread;
         return w;
     };
 
     // ---- this lane's row: (group g, batch b, point n)
-    const unsigned R = (unsigned)slab * 32u + (unsigned)r;
-    const bool valid = R < (unsigned)A.M;
-    const unsigned g = valid ? R / (unsigned)A.K : 0u;
+    unsigned g;
+    bool valid;
+    int n, urow_e = -1;
+    if (compact) {
+        // unit i of the workgroup = rows 8(i%4).. of wave i/4; a row past the unit's distinct
+        // neighbours takes the unit's first (a distinct neighbour of the same group)
+        urow_e = A.cunits[blockIdx.x * kUnitsPerWG + wave * 4 + (r >> 3)];
+        valid = urow_e >= 0;
+        const int k = (urow_e >> 4) & 15, nv = (urow_e & 7) + 1;
+        g = valid ? c_g0 + (unsigned)(urow_e >> 8) : c_g0;
+        const int j = kUnitRows * k + ((r & 7) < nv ? (r & 7) : 0);
+        n = valid ? (int)s.idx[(int64_t)g * A.K + j] : 0;
+    } else {
+        const unsigned R = (unsigned)slab * 32u + (unsigned)r;
+        valid = R < (unsigned)A.M;
+        g = valid ? R / (unsigned)A.K : 0u;
+        n = valid ? (int)s.idx[R] : 0;
+    }
     const unsigned b = g / (unsigned)A.S;
-    const int n = valid ? (int)s.idx[R] : 0;
     const float *frow = s.feat ? s.feat + (int64_t)b * s.fb + (int64_t)n * s.fn : nullptr;
     const float *prow = s.pts + (int64_t)b * s.pb + (int64_t)n * s.pn;
     const float *crow = s.ctr + (int64_t)g * A.C;
@@ -292,7 +333,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         // ---- layer 0 pre-transformed: acc = z[point] - u[group], already in the transposed
         // accumulator layout (register 4m + i of lane (r, h) = channel 32t + 8m + 4h + i)
 #pragma unroll
-        for (int st = 0; st < kStages - 1; ++st) issue_stage(st);
+        for (int st = 0; st < KS - 1; ++st) issue_stage(st);
         const float *zrow = A.z + ((int64_t)b * s.N + n) * (32 * T0);
         const float *urow = ulds + (int)(g - g0) * (32 * T0);
         // Tile t+1's z / u loads are issued while tile t is split (one tile of lookahead).  The
@@ -347,7 +388,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             }
         }
 #pragma unroll
-        for (int st = 0; st < kStages - 1; ++st) issue_stage(st);  // overlaps the gather's latency
+        for (int st = 0; st < KS - 1; ++st) issue_stage(st);  // overlaps the gather's latency
         cfloatx16 acc[T0];
 #pragma unroll
         for (int t = 0; t < T0; ++t)
@@ -386,7 +427,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
         // layer 0's loads are all consumed: start the ring, then the epilogue hides its latency
 #pragma unroll
-        for (int st = 0; st < kStages - 1; ++st) issue_stage(st);
+        for (int st = 0; st < KS - 1; ++st) issue_stage(st);
 #pragma unroll
         for (int t = 0; t < T0; ++t) {
             hidden_epilogue<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
@@ -427,7 +468,37 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         const float al = al2[col], be = be2[col];
         const bool up = al >= 0.f;
         auto fin = [&](float mx, float mn) { return chain_relu(__builtin_fmaf(up ? mx : mn, al, be)); };
-        if (A.K == 8 || A.K == 16) {
+        if (compact) {
+            // one max per 8-row unit (registers 4k..4k+3 of both halves); consecutive units of a
+            // group merged in registers, then into the workgroup's LDS pool (ds_max_u32; ReLU
+            // outputs >= +0: uint order == float order).  No global write inside the ring's
+            // loop: its counted vmcnt waits would also wait for them.
+            float smx = 0.f, smn = 0.f;
+            int sg = -1;
+            auto flush = [&]() {
+                if (sg >= 0 && h == 0)
+                    atomicMax(&cpool[sg * coutL + col], __float_as_uint(fin(smx, smn)));
+            };
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int ue = __builtin_amdgcn_readlane(urow_e, 8 * k);  // uniform
+                if (ue < 0) break;  // units are used in order: the rest of the slab is unused
+                float mx = fmaxf(fmaxf(acc[4 * k], acc[4 * k + 1]), fmaxf(acc[4 * k + 2], acc[4 * k + 3]));
+                float mn = fminf(fminf(acc[4 * k], acc[4 * k + 1]), fminf(acc[4 * k + 2], acc[4 * k + 3]));
+                mx = fmaxf(mx, swap_halves(mx));
+                mn = fminf(mn, swap_halves(mn));
+                if ((ue >> 8) != sg) {
+                    flush();
+                    sg = ue >> 8;
+                    smx = mx;
+                    smn = mn;
+                } else {
+                    smx = fmaxf(smx, mx);
+                    smn = fminf(smn, mn);
+                }
+            }
+            flush();
+        } else if (A.K == 8 || A.K == 16) {
             float mx[4], mn[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {  // rows 8k..8k+7 of the slab: registers 4k..4k+3, both halves
@@ -472,7 +543,19 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing (repeat) copies
-    if (A.pool_mode == 1) {
+    if (compact) {
+        __syncthreads();
+        // a group shared with the neighbouring workgroup is merged by atomicMax into its row
+        // (zeroed by compact_scan_kernel); the others are stored
+        for (int e = tid; e < c_ng * coutL; e += 64 * kChainWaves) {
+            const int gl = e / coutL, c = e - gl * coutL;
+            float *o = A.out + (int64_t)(c_g0 + (unsigned)gl) * A.ostride + c;
+            if ((gl == 0 && (c_flags & 1)) || (gl == c_ng - 1 && (c_flags & 2)))
+                atomicMax(reinterpret_cast<unsigned *>(o), cpool[e]);
+            else
+                *o = __uint_as_float(cpool[e]);
+        }
+    } else if (A.pool_mode == 1) {
         __syncthreads();
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) {
             const int gl = e / coutL, c = e - gl * coutL;
@@ -561,12 +644,110 @@ extern "C" int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t c
     return PN2_OK;
 }
 
-// ------------------------------------------------------------------ host: dispatch
+// ------------------------------------------------------------------ compact neighbourhoods
 namespace pn2 {
+
+// One workgroup per cloud: every group's 8-row units (its distinct-neighbour count from the
+// ball query, pn2_ball_query_cnt_f32, rounded up to whole units) laid out in group order (an
+// exclusive scan), 16 units per chain workgroup; the workgroup descriptors and unit table the
+// chain kernel reads; and a zeroed output row for every group whose units span two workgroups
+// (merged there by atomicMax).
+constexpr int kScanThreads = 1024;
+
+__global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
+    const int *__restrict__ cnt, int S, int K, int wpc, int *__restrict__ units,
+    int2 *__restrict__ desc, float *__restrict__ out, int64_t ostride, int cout) {
+    extern __shared__ int ssm[];
+    int *st = ssm;            // [S] units of group s, then its first unit
+    int *strad = st + S;      // [S] groups to zero
+    int *glo = strad + S;     // [wpc] first group of each workgroup
+    int *wsum = glo + wpc;    // [16] wave totals, [16] straddler count
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x;
+    const int *cb = cnt + (int64_t)b * S;
+    const int per = (S + kScanThreads - 1) / kScanThreads;
+    const int lo = min(S, tid * per), hi = min(S, lo + per);
+    int sum = 0;
+    for (int i = lo; i < hi; ++i) {
+        const int u = max(1, (cb[i] + kUnitRows - 1) / kUnitRows);
+        st[i] = u;
+        sum += u;
+    }
+    if (tid == 0) wsum[16] = 0;
+    // exclusive scan of the per-thread sums: within each wave, then over the 16 wave totals
+    int inc = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(inc, off);
+        if (lane >= off) inc += v;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    int wpre = 0, total = 0;
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+        const int t = wsum[w];
+        if (w < wave) wpre += t;
+        total += t;
+    }
+    int run = wpre + inc - sum;
+    for (int i = lo; i < hi; ++i) {
+        const int u = st[i];
+        st[i] = (run << 8) | u;
+        run += u;
+    }
+    __syncthreads();
+    // the first group of every workgroup (the one holding unit 16w) and the groups that span two
+    for (int i = tid; i < S; i += kScanThreads) {
+        const int s0 = st[i] >> 8, en = s0 + (st[i] & 255) - 1;
+        for (int w = (s0 + kUnitsPerWG - 1) / kUnitsPerWG; w * kUnitsPerWG <= en; ++w) glo[w] = i;
+        if (s0 / kUnitsPerWG != en / kUnitsPerWG) strad[atomicAdd(&wsum[16], 1)] = i;
+    }
+    __syncthreads();
+    for (int w = tid; w < wpc; w += kScanThreads) {
+        int2 d = make_int2(0, -1);
+        if (w * kUnitsPerWG < total) {
+            const int g = glo[w];
+            // last group: the one holding the workgroup's last used unit
+            const int lu = min((w + 1) * kUnitsPerWG, total) - 1;
+            int l = g;
+            while (l + 1 < S && (st[l + 1] >> 8) <= lu) ++l;
+            const int first = (st[g] >> 8) < w * kUnitsPerWG ? 1 : 0;
+            const int last = (st[l] >> 8) + (st[l] & 255) > (w + 1) * kUnitsPerWG ? 2 : 0;
+            d = make_int2(g, (l - g + 1) | ((first | last) << 8));
+        }
+        desc[(int64_t)b * wpc + w] = d;
+    }
+    int *ub = units + (int64_t)b * wpc * kUnitsPerWG;
+    for (int u = total + tid; u < wpc * kUnitsPerWG; u += kScanThreads) ub[u] = -1;
+    for (int i = tid; i < S; i += kScanThreads) {
+        const int s0 = st[i] >> 8, nu = st[i] & 255;
+        for (int k = 0; k < nu; ++k) {
+            // rows past the distinct ones inside a unit are the group's padding (repeats of its
+            // first neighbour); only rows past K (K % 8 != 0) are cut
+            const int u = s0 + k, nv = min(kUnitRows, K - kUnitRows * k);
+            ub[u] = ((i - glo[u / kUnitsPerWG]) << 8) | (k << 4) | ((k == nu - 1) << 3) | (nv - 1);
+        }
+    }
+    const int ns = wsum[16];
+    for (int e = tid; e < ns * cout; e += kScanThreads) {
+        const int j = e / cout, c = e - j * cout;
+        out[((int64_t)b * S + strad[j]) * ostride + c] = 0.f;
+    }
+}
+
+// ------------------------------------------------------------------ host: dispatch
+
+static int compact_stages() {
+    const char *e = getenv("PN2_COMPACT_KS");
+    return (e && strcmp(e, "3") == 0) ? 3 : 2;
+}
 
 template <int T0, int T1, int KB0M, int NP>
 static int launch_chain_sig(const ChainArgs &A, unsigned grid, size_t lds, hipStream_t st) {
-    hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
+    if (A.pool_mode == 3 && compact_stages() == 2)
+        hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP, 2>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
+    else
+        hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP, kStages>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
     PN2_LAUNCH_CHECK("sa_chain_kernel");
     return PN2_OK;
 }
@@ -619,12 +800,37 @@ static bool chain_shape(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nl
     return kbs[0] >= 1;
 }
 
+// compact neighbourhoods (pool_mode 3): groups of K in [9, 128] (K <= 8 is one unit anyway),
+// given the ball query's counts, the scan kernel's LDS within one CU's 160 KB.  PN2_COMPACT=0
+// disables (A/B), =1 also compacts pre-pass chains; PN2_COMPACT_KS=3 keeps the 3-stage ring.
+static int64_t compact_wpc(const pn2_sa_src &s) {
+    return (s.S * ((s.K + kUnitRows - 1) / kUnitRows) + kUnitsPerWG - 1) / kUnitsPerWG;
+}
+static size_t compact_scan_lds(const pn2_sa_src &s) {
+    return (size_t)(2 * s.S + compact_wpc(s) + 32) * 4;
+}
+static bool chain_use_compact(const pn2_sa_src &s) {
+    if (!s.cnt || s.K <= kUnitRows || s.K > 128 || s.S < 1) return false;
+    if (compact_scan_lds(s) > (size_t)160 * 1024) return false;
+    if (const char *e = getenv("PN2_COMPACT"))
+        if (strcmp(e, "0") == 0) return false;
+    return true;
+}
+static int64_t compact_table_bytes(const pn2_sa_src &s) {
+    return s.B * compact_wpc(s) * (kUnitsPerWG * 4 + 8);
+}
+
+// workspace of a chain launch: [layer-0 pre-pass z | compact unit table | compact descriptors]
 int64_t chain_prepass_bytes(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np) {
     int T0, T1, kbs[3];
     if (!chain_shape(s, layers, nlayers, 1, T0, T1, kbs)) return 0;
+    if (chain_kb0m(T0, T1, kbs[0]) < 0) return 0;
     const int64_t M = s.B * s.S * s.K;
-    if (!chain_use_prepass(s, layers, T0, T1, kbs[0], M, np)) return 0;
-    return s.B * s.N * layers[0].cout * 4;
+    int64_t bytes = 0;
+    if (chain_use_prepass(s, layers, T0, T1, kbs[0], M, np))
+        bytes += (s.B * s.N * layers[0].cout * 4 + 15) / 16 * 16;
+    if (chain_use_compact(s)) bytes += compact_table_bytes(s);
+    return bytes;
 }
 
 // 1: launched, 0: this chain is not eligible (caller uses the fp32 kernels), <0: error
@@ -638,13 +844,43 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     if (!chain_shape(s, layers, nlayers, pool, T0, T1, kbs)) return 0;
     int KB0M = chain_kb0m(T0, T1, kbs[0]);
     if (KB0M < 0) return 0;
-    const int64_t zbytes = s.B * s.N * layers[0].cout * 4;
+    // without compaction a 32-row slab must hold rows of one group (K = 8, 16: several whole
+    // groups; K % 32 == 0: part of one)
+    if (!(pool && chain_use_compact(s)) && !(K == 8 || K == 16 || K % 32 == 0)) return 0;
+    const int64_t zbytes = (s.B * s.N * layers[0].cout * 4 + 15) / 16 * 16;
     const bool pre = chain_use_prepass(s, layers, T0, T1, kbs[0], M, np) && ws &&
                      ws_bytes >= zbytes && ((uintptr_t)ws & 15) == 0;
+    const int64_t zb = pre ? zbytes : 0;
+    bool compact = pool && chain_use_compact(s) && ws && ((uintptr_t)ws & 15) == 0 &&
+                   ws_bytes >= zb + compact_table_bytes(s);
+    // With the layer-0 pre-pass (wide first layers: SSG / pose sa2) the group pool and the u
+    // table of a compact launch cost a weight-ring stage or an occupancy step, which measured
+    // slower than computing the padding rows (SSG sa2: 143 / 160 us vs 131 us): compact only
+    // without it unless PN2_COMPACT=1.
+    if (pre) {
+        const char *e = getenv("PN2_COMPACT");
+        if (!(e && strcmp(e, "1") == 0)) compact = false;
+    }
     if (pre) {
         const int rc = launch_layer0_prepass(s, layers[0], ws, st);
         if (rc != PN2_OK) return rc;
         KB0M = -1;
+    }
+    const int wpc = compact ? (int)compact_wpc(s) : 0;
+    int *cunits = nullptr;
+    int2 *cdesc = nullptr;
+    if (compact) {
+        cunits = reinterpret_cast<int *>(reinterpret_cast<char *>(ws) + zb);
+        cdesc = reinterpret_cast<int2 *>(cunits + s.B * wpc * kUnitsPerWG);
+        const size_t slds = compact_scan_lds(s);
+        static const hipError_t attr = hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&compact_scan_kernel),
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)attr;
+        hipLaunchKernelGGL(compact_scan_kernel, dim3((unsigned)s.B), dim3(kScanThreads), slds, st,
+                           s.cnt, (int)s.S, (int)s.K, wpc, cunits, cdesc, out, ostride,
+                           (int)layers[2].cout);
+        PN2_LAUNCH_CHECK("compact_scan_kernel");
     }
     ChainArgs A;
     memset(&A, 0, sizeof(A));
@@ -665,6 +901,9 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     A.ostride = ostride;
     A.vec_feat = (s.D > 0 && s.D % 4 == 0 && ((uintptr_t)s.feat & 15) == 0 && s.fn % 4 == 0 &&
                   s.fb % 4 == 0) ? 1 : 0;
+    A.cunits = cunits;
+    A.cdesc = cdesc;
+    A.wpc = wpc;
     if (pre) {
         A.z = ws;
         A.w0x = layers[0].wt;
@@ -672,7 +911,10 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     }
     const int64_t coutL = layers[2].cout;
     size_t lds = 0;
-    if (K == 8 || K == 16 || K == 32) {
+    if (compact) {
+        A.pool_mode = 3;
+        lds = (size_t)kUnitsPerWG * coutL * 4;
+    } else if (K == 8 || K == 16 || K == 32) {
         A.pool_mode = 0;
     } else if (kChainRows % K == 0) {
         A.pool_mode = 1;
@@ -680,7 +922,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     } else {
         A.pool_mode = 2;
     }
-    if (lds > 32 * 1024) A.pool_mode = 2, lds = 0;
+    if (lds > 32 * 1024 && !compact) A.pool_mode = 2, lds = 0;
     if (A.pool_mode == 2) {
         const int64_t G = M / K;
         hipError_t e = (ostride == coutL)
@@ -688,14 +930,14 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
                            : hipMemset2DAsync(out, (size_t)ostride * 4, 0, (size_t)coutL * 4, (size_t)G, st);
         if (e != hipSuccess) return set_error(PN2_EHIP, "sa_chain: memset: %s", hipGetErrorString(e));
     }
-    const unsigned grid = (unsigned)((M + kChainRows - 1) / kChainRows);
+    const unsigned grid = compact ? (unsigned)(s.B * wpc) : (unsigned)((M + kChainRows - 1) / kChainRows);
     // LDS: [pool][BN scale/shift][per-wave rings]
     A.lds_bn = (int)((lds + 15) / 16 * 16);
     const size_t bn_bytes = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + coutL);
     A.lds_ring = (int)((A.lds_bn + bn_bytes + 15) / 16 * 16);
-    lds = (size_t)A.lds_ring + (size_t)kStages * (np == 3 ? stage_bytes<3>() : stage_bytes<1>());
+    lds = (size_t)A.lds_ring + (size_t)(compact ? compact_stages() : kStages) * (np == 3 ? stage_bytes<3>() : stage_bytes<1>());
     if (pre) {  // u for every group a workgroup's rows touch
-        A.u_groups = (int)((kChainRows + K - 1) / K + 1);
+        A.u_groups = compact ? kUnitsPerWG : (int)((kChainRows + K - 1) / K + 1);
         A.lds_u = (int)((lds + 15) / 16 * 16);
         lds = (size_t)A.lds_u + (size_t)A.u_groups * layers[0].cout * 4;
     }

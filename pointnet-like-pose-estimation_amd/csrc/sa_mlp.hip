@@ -934,7 +934,7 @@ extern "C" int64_t pn2_sa_mlp_workspace_bytes_bf16(const pn2_sa_src *src,
     int64_t M = 0, K = 1;
     if (validate(src, layers, nlayers, M, K) != PN2_OK) return -1;
     const int64_t ds = nlayers > 1 ? dense_split_width(*src, layers, nlayers, 1) : 0;
-    return 2 * M * ds * 4;
+    return std::max(2 * M * ds * 4, chain_prepass_bytes(*src, layers, nlayers, 1));
 }
 
 extern "C" int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers,

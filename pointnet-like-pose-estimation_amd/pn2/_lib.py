@@ -39,6 +39,7 @@ class SaSrc(ctypes.Structure):
         ("idx", _vp),
         ("rows", _vp), ("rs", _i64),
         ("B", _i64), ("N", _i64), ("C", _i64), ("D", _i64), ("S", _i64), ("K", _i64),
+        ("cnt", _vp),
     ]
 
 
@@ -60,6 +61,7 @@ SIGNATURES = {
     "pn2_fps_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "pn2_pack_points_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pn2_ball_query_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp]),
+    "pn2_ball_query_cnt_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp, _vp]),
     "pn2_square_distance_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pn2_index_points_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp]),
     "pn2_group_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
@@ -95,7 +97,7 @@ SIGNATURES = {
                                    _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 _lib = None
 
 

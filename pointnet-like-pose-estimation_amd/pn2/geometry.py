@@ -114,7 +114,8 @@ _tls = threading.local()
 @contextlib.contextmanager
 def provide(entries):
     """entries: {id(module): (input data_ptr, new_points, ctr_packed, pts_packed, idxs)};
-    idxs: the ball-query indices per radius of the module, or None (the module queries)."""
+    idxs: the ball query's (indices, distinct-neighbour counts) per radius of the module, or
+    None (the module queries)."""
     prev = getattr(_tls, "entries", None)
     _tls.entries = entries
     try:

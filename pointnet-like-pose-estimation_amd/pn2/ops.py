@@ -175,8 +175,11 @@ def _(points):
 
 
 # ------------------------------------------------------------------------------ ball query
-def ball_query_direct(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, nsample: int) -> Tensor:
-    """Packed points [B,N,cp] and centroids [B,S,cp] -> group_idx [B,S,nsample] int64."""
+def ball_query_direct(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, nsample: int,
+                      with_count: bool = False):
+    """Packed points [B,N,cp] and centroids [B,S,cp] -> group_idx [B,S,nsample] int64, and with
+    with_count also the distinct neighbours per centroid, [B,S] int32 (entries past them repeat
+    entry 0; sa_mlp_max_direct(cnt=...) then computes only those rows)."""
     _dev(pts_packed, "pn2::ball_query")
     B, N, _ = pts_packed.shape
     S = ctr_packed.shape[1]
@@ -184,15 +187,20 @@ def ball_query_direct(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: fl
         # the reference's `group_idx[mask] = group_first[mask]` fails the same way (:89)
         raise IndexError("query_ball_point: sample_number %d > number of points %d" % (nsample, N))
     out = torch.empty(B, S, nsample, dtype=torch.int64, device=pts_packed.device)
+    cnt = torch.empty(B, S, dtype=torch.int32, device=pts_packed.device) if with_count else None
     cp = pts_packed.shape[2]
-    _run("pn2_ball_query_f32", _L.pn2_ball_query_f32,
+    _run("pn2_ball_query_f32", _L.pn2_ball_query_cnt_f32,
          (pts_packed.data_ptr(), ctr_packed.data_ptr(), B, N, S, C, float(radius), nsample,
-          out.data_ptr(), _stream(pts_packed)), pts_packed.device,
-         nbytes=4.0 * cp * B * (N + S) + 8.0 * B * S * nsample)
-    return out
+          out.data_ptr(), 0 if cnt is None else cnt.data_ptr(), _stream(pts_packed)),
+         pts_packed.device, nbytes=4.0 * cp * B * (N + S) + 8.0 * B * S * nsample)
+    return (out, cnt) if with_count else out
 
 
-ball_query = torch.library.custom_op("pn2::ball_query", ball_query_direct, mutates_args=())
+def _ball_query_op(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, nsample: int) -> Tensor:
+    return ball_query_direct(pts_packed, ctr_packed, C, radius, nsample)
+
+
+ball_query = torch.library.custom_op("pn2::ball_query", _ball_query_op, mutates_args=())
 
 
 @ball_query.register_fake
@@ -338,8 +346,12 @@ def _(weight, xyz, xyz_first):
 
 
 # ------------------------------------------------------------------------------ sa_mlp_max_
-def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K):
+def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K, cnt=None):
     s = SaSrc()
+    if cnt is not None:
+        if cnt.dtype != torch.int32 or not cnt.is_contiguous() or cnt.numel() != B * S:
+            raise ValueError("pn2::sa_mlp_max_: cnt must be a contiguous int32 [B, S] tensor")
+        s.cnt = cnt.data_ptr()
     s.mode = mode
     if points is not None:
         s.pts = points.data_ptr()
@@ -364,7 +376,8 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
                 centers: Optional[Tensor], idx: Optional[Tensor], wts: List[Tensor],
                 alphas: List[Tensor], betas: List[Tensor], cins: List[int],
                 splits: List[Tensor], precision: str = "fp32", flags: Optional[List[int]] = None,
-                rows: Optional[Tensor] = None, pool: bool = True) -> None:
+                rows: Optional[Tensor] = None, pool: bool = True,
+                cnt: Optional[Tensor] = None) -> None:
     """Fused gather -> MLP (conv1x1+BN+ReLU)* -> max over each group, written channels-last
     into `out` ([G, >=cout] view with unit column stride; G = B*S groups, or B for
     group_all).  mode: 0 SSG grouping, 1 MSG grouping, 2 group_all, 3 rows (`rows` [B, R, cin]
@@ -372,7 +385,9 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
     pack_layer_split images of the same layers (empty list: fp32 kernels only).
     precision: "fp32" (pn2_sa_mlp_max_f32) or "bf16" (pn2_sa_mlp_max_bf16, needs splits).
     flags: per-layer PN2_LAYER_* bits (LAYER_NO_RELU).  pool=False: `out` gets every row's
-    last-layer output ([M, >=cout], group_all / rows sources)."""
+    last-layer output ([M, >=cout], group_all / rows sources).  cnt: the ball query's
+    distinct-neighbour counts ([B, S] int32, grouping modes) -- only those rows of each group are
+    computed (the rest repeat the first neighbour; same result)."""
     if precision not in PRECISIONS:
         raise ValueError("pn2::sa_mlp_max_: precision must be one of %s" % (PRECISIONS,))
     bf16 = precision == "bf16"
@@ -398,7 +413,8 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
             S, K = idx.shape[1], idx.shape[2]
             idx = idx.contiguous()
             centers = centers.contiguous()
-        src = _src(mode, points, feature, centers, idx, None, B, N, C, D, S, K)
+        src = _src(mode, points, feature, centers, idx, None, B, N, C, D, S, K,
+                   cnt if mode in (_lib.SRC_GROUP_XYZ_FIRST, _lib.SRC_GROUP_FEAT_FIRST) else None)
         dev_t = points
     n = len(wts)
     layers = (MlpLayer * n)()
@@ -430,7 +446,7 @@ sa_mlp_max_ = torch.library.custom_op("pn2::sa_mlp_max_", sa_mlp_max_direct, mut
 
 @sa_mlp_max_.register_fake
 def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits, precision="fp32",
-      flags=None, rows=None, pool=True):
+      flags=None, rows=None, pool=True, cnt=None):
     return None
 
 

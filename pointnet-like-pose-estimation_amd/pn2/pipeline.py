@@ -223,7 +223,7 @@ class PipelinedForward:
                     rk = list(zip(sa.radius_list, sa.sample_number_list))
                 else:
                     rk = [(sa.radius, sa.sample_number)]
-                idxs = [ops.ball_query_direct(ppk, cpk, C, r, kk) for r, kk in rk]
+                idxs = [ops.ball_query_direct(ppk, cpk, C, r, kk, True) for r, kk in rk]
                 entries[id(sa)] = (p.data_ptr(), newp, cpk, ppk, idxs)
                 p = newp
         return entries
@@ -272,7 +272,7 @@ class PipelinedForward:
                         nxt_ev = geo.record_event()
                 main.wait_event(ev)
                 for _, newp, cpk, ppk, idxs in entries.values():
-                    for t in [newp, cpk, ppk] + idxs:
+                    for t in [newp, cpk, ppk] + [t for ic in idxs for t in ic]:
                         t.record_stream(main)
                 with torch.cuda.stream(main), geometry.provide(entries):
                     extra = () if extras is None else tuple(extras[i])
@@ -337,10 +337,10 @@ class GraphedPipeline(PipelinedForward):
     Events order the slot reuse: batch i+nslots's fps waits until batch i's sa and head graphs
     and the output clone have run (it overwrites the slot's inputs and geometry outputs, which
     a group_all layer in the head graph still reads), batch i+nslots's sa waits for batch i's
-    head (they share a memory pool).  With 3 slots (default) the geometry chain has two batches of slack: at SSG
-    its ~340 us (under MLP contention) is as long as the compute stream's work, so with 2 slots
-    any jitter on either stream stalls the other.  Static memory makes the tail safe for every head here, including the translation
-    heads' ``mean`` (see PipelinedForward).
+    head (they share a memory pool).  A slot's fps -> sa -> head is thus a dependency cycle that
+    nslots batches must cover: 4 slots (default) measured 84.5-84.9k clouds/s at SSG against
+    74-77k with 3 (5 and 6 within noise of 4).  Static memory makes the tail safe for every
+    head here, including the translation heads' ``mean`` (see PipelinedForward).
 
     RNG and results: as PipelinedForward.  The first batch of a new input signature (or after
     any parameter change) runs through the eager pipeline -- its real result, its draws -- and
@@ -361,7 +361,7 @@ class GraphedPipeline(PipelinedForward):
     compute stream (59.5k).
     """
 
-    def __init__(self, model, geometry_cus=0, tail=True, nslots=3, geometry_streams=2):
+    def __init__(self, model, geometry_cus=0, tail=True, nslots=4, geometry_streams=2):
         super().__init__(model, geometry_cus, bool(tail))
         if nslots < 2:
             raise ValueError("pn2.pipeline: GraphedPipeline needs at least 2 slots")
@@ -449,6 +449,17 @@ class GraphedPipeline(PipelinedForward):
             if handle is not None:
                 handle.remove()
         torch.cuda.synchronize(dev)
+        # does anything after the sa graph read the fps graph's outputs?  The head graph does
+        # when it holds a layer (a trailing group_all reads the split layer's centroids); the
+        # output clone does when the model returns one of them
+        geo = set()
+        for _, newp, cpk, ppk, idxs in sl.entries.values():
+            geo.update(t.untyped_storage().data_ptr()
+                       for t in [newp, cpk, ppk] + [t for ic in idxs for t in ic])
+        outs = sl.out if isinstance(sl.out, (tuple, list)) else (sl.out,)
+        flat = [t for o in outs for t in (o if isinstance(o, (tuple, list)) else (o,))]
+        sl.tail_reads_geometry = (self.tail and self._split_index() < len(self.sas) - 1) or any(
+            isinstance(t, torch.Tensor) and t.untyped_storage().data_ptr() in geo for t in flat)
         return sl
 
     def run(self, batches, extras=None, post=None):
@@ -544,7 +555,7 @@ class GraphedPipeline(PipelinedForward):
                     out = _clone(sl.out)
                     # recorded before `post` (e.g. an all_gather) so the next fps replay of
                     # this slot does not wait for the collective
-                    ev_read[s] = ts.record_event()
+                    ev_read[s] = ts.record_event() if sl.tail_reads_geometry else ev_sa[s]
                     if post is not None:
                         out = post(i, out)
                     ev_head[s] = ts.record_event()

@@ -276,15 +276,15 @@ class PointNetSetAbstraction(nn.Module):
         pre = geometry.take(self, pts)  # FPS (+ ball query) precomputed by pn2.pipeline
         if pre is not None:
             new_points, cpk, ppk, idxs = pre
-            idx = idxs[0] if idxs else ops.ball_query_direct(ppk, cpk, C, self.radius, K)
+            idx, cnt = idxs[0] if idxs else ops.ball_query_direct(ppk, cpk, C, self.radius, K, True)
         else:
             with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
                 _, new_points, cpk, ppk = ops.fps_direct(pts, S, _draw_start(B, N, dev))
-                idx = ops.ball_query_direct(ppk, cpk, C, self.radius, K)
-            span.finish([new_points], [new_points, idx])
+                idx, cnt = ops.ball_query_direct(ppk, cpk, C, self.radius, K, True)
+            span.finish([new_points], [new_points, idx, cnt])
         out = torch.empty(B * S, cout, device=dev, dtype=torch.float32)
         ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
-                        cins, splits, _precision(self))
+                        cins, splits, _precision(self), cnt=cnt)
         return _inference_outputs(self, new_points.permute(0, 2, 1),
                                   out.view(B, S, cout).permute(0, 2, 1))
 
@@ -343,22 +343,22 @@ class PointNetSetAbstractionMsg(nn.Module):
         if pre is not None:
             new_points, cpk, ppk, idxs = pre
             if not idxs:
-                idxs = [ops.ball_query_direct(ppk, cpk, C, r, k)
+                idxs = [ops.ball_query_direct(ppk, cpk, C, r, k, True)
                         for r, k in zip(self.radius_list, self.sample_number_list)]
         else:
             with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
                 _, new_points, cpk, ppk = ops.fps_direct(pts, S, _draw_start(B, N, dev))
-                idxs = [ops.ball_query_direct(ppk, cpk, C, r, k)
+                idxs = [ops.ball_query_direct(ppk, cpk, C, r, k, True)
                         for r, k in zip(self.radius_list, self.sample_number_list)]
-            span.finish([new_points], [new_points] + idxs)
+            span.finish([new_points], [new_points] + [t for ic in idxs for t in ic])
         out = torch.empty(B * S, total, device=dev, dtype=torch.float32)
         prec = _precision(self)
         col = 0
-        for i, idx in enumerate(idxs):
+        for i, (idx, cnt) in enumerate(idxs):
             wts, als, bes, cins, splits = chains[i]
             cout = wts[-1].shape[1]
             ops.sa_mlp_max_direct(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
-                            new_points, idx, wts, als, bes, cins, splits, prec)
+                            new_points, idx, wts, als, bes, cins, splits, prec, cnt=cnt)
             col += cout
         return _inference_outputs(self, new_points.permute(0, 2, 1),
                                   out.view(B, S, total).permute(0, 2, 1))

@@ -123,6 +123,68 @@ def test_sa_mlp_deterministic(case):
         np.testing.assert_array_equal(o, outs[0])
 
 
+# compact neighbourhoods (sa_chain.hip pool_mode 3): (C, D, K, S, N, radius, mlp, msg)
+COMPACT = [
+    (3, 0, 32, 512, 1024, 0.2, [64, 64, 128], False),     # SSG sa1 (about half the rows)
+    (3, 128, 64, 128, 512, 0.4, [128, 128, 256], False),  # SSG sa2: pre-pass + compact
+    (3, 0, 12, 64, 512, 0.3, [64, 64, 128], False),       # K % 8 != 0
+    (3, 0, 72, 40, 256, 2.0, [64, 64, 128], False),       # full groups of 9 units: straddling
+    (3, 0, 128, 32, 512, 0.5, [64, 64, 128], False),      # up to 16 units per group
+    (3, 13, 16, 64, 512, 0.1, [32, 32, 64], True),        # MSG row order, unaligned features
+    (10, 0, 32, 256, 2048, 0.2, [64, 64, 128], False),    # pose layout
+]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", range(len(COMPACT)))
+def test_compact_neighbourhoods_bit_exact(case, prec, monkeypatch):
+    """Computing only each group's distinct rows (8-row units, the padding repeats of the first
+    neighbour dropped) gives the bits of the full K rows per group: every row's MLP is
+    computed the same way, and the max is the same without repeats.  Covers K % 8 != 0, groups
+    spanning two workgroups (merged by atomicMax into rows the scan zeroed), up to 16 units per
+    group, MSG, the pose layout, and bf16; the fp32 result also against the float64 oracle."""
+    import pn2
+    C, D, K, S, N, radius, mlp, msg = COMPACT[case]
+    B = 3
+    pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 500 + case)
+    gen = torch.Generator().manual_seed(600 + case)
+    feat = torch.randn(B, N, D, generator=gen) if D else None
+    torch.manual_seed(case)
+    if msg:
+        sa = pn2.PointNetSetAbstractionMsg(S, [K], [radius], D, [mlp])
+        convs, bns = sa.conv_blocks[0], sa.bn_blocks[0]
+    else:
+        sa = pn2.PointNetSetAbstraction(S, K, radius, C + D, mlp)
+        convs, bns = sa.mlp_convs, sa.mlp_bns
+    cases.randomize_bn(sa, case)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous().to(DEV)
+    f = feat.permute(0, 2, 1).contiguous().to(DEV) if D else None
+    outs = {}
+    chainable = K in (8, 16) or K % 32 == 0
+    for mode in ("0", "1") if (chainable or prec == "fp32") else ("1",):
+        monkeypatch.setenv("PN2_COMPACT", mode)
+        torch.manual_seed(77)
+        with torch.no_grad(), pn2.mlp_precision(prec):
+            outs[mode] = sa(x, f)[1].cpu().numpy()
+    if chainable:  # else the full-row launch is not the chain kernel (no bf16 kernel at all)
+        np.testing.assert_array_equal(outs["1"].view(np.uint32), outs["0"].view(np.uint32))
+    if prec == "fp32" or not chainable:
+        ps = pts.permute(0, 2, 1).contiguous().permute(0, 2, 1)
+        torch.manual_seed(77)
+        start = torch.randint(0, N, (B,), dtype=torch.long)
+        ctr = oracle.index_points(ps, oracle.farthest_point_sample(ps, S, start))
+        idx = oracle.query_ball_point(radius, K, ps, ctr)
+        want = oracle.mlp_max(oracle.group(ps, feat, idx, ctr, feature_first=msg),
+                              _oracle_layers(convs, bns))
+        for mode in outs:
+            got = outs[mode].transpose(0, 2, 1)
+            if prec == "fp32":
+                _close(got, want)
+            else:  # bf16 operands: 2e-2 of the output's max magnitude
+                assert np.abs(got - want).max() <= 2e-2 * np.abs(want).max()
+
+
 # group_all SA layers (sample_and_group_all + MLP + max over every point, pointnet2_utils.py
 # :122-141, :163-172): (C, D, N points = K, mlp, split kernel expected)
 GROUP_ALL = [
