@@ -2,96 +2,218 @@
 //
 // Replaces query_ball_point (/root/reference/model/pointnet2_utils.py:70-90) including the
 // square_distance it calls (pointnet2_utils.py:5-26).  The reference materialises the full
-// [B,S,N] distance matrix, masks it and SORTS every row to find the first K in-radius indices;
-// here one wave owns one centroid and streams the cloud in index order, 64 points per step:
-//   d = ((-2 * fma-chain(ctr . p)) + ssq(ctr)) + ssq(p)     (MKL sgemm + ATen sum order;
-//       unfused mul/add chain when S*N*C < 400: ATen's naive small-bmm kernel)
-//   hit = !(d > (float)(r*r))                                (the reference's masking test)
-//   ballot -> popcount prefix -> ordered compaction, early exit once K hits are found.
-// No [B,S,N] tensor exists.  Points come from the packed [B][N][cp] records
-// (coords, ssq, pad) so one lane's point is one or three 16-byte loads.
+// [B,S,N] distance matrix, masks it and SORTS every row to find the first K in-radius indices.
+// Here no [B,S,N] tensor exists.
+//
+// Mapping: the 64 lanes of a wave are 64 consecutive centroids of one cloud (a centroid's
+// record lives in the lane's registers); the P waves of a workgroup share those centroids and
+// split the cloud into consecutive segments of TS points.  The cloud is scanned in rounds of
+// P*TS points: the workgroup stages the round's packed records (coords, ssq, pad) in LDS with
+// coalesced 16-byte loads, then every wave reads its segment back at wave-uniform addresses
+// (one broadcast ds_read_b128 per xyz point, 8 in flight) and tests each point against its
+// 64 centroids:
+//     d = ((-2 * fma-chain(ctr . p)) + ssq(ctr)) + ssq(p)   (MKL sgemm + ATen sum order;
+//         unfused mul/add chain when S*N*C < 400: ATen's naive small-bmm kernel)
+//     hit = !(d > (float)(r*r))                              (the reference's masking test)
+// A lane accumulates its hits as one bitmask word per 32 points (shift + or, no branch).
+// After the scan the per-(segment, centroid) hit counts go through LDS; a lane's prefix over
+// the earlier segments and rounds is the output slot of its first hit in the segment, so the
+// hits are written in index order ("first K in index order") with no sort.  The workgroup
+// stops after the round in which every one of its centroids reached K hits.  Padding (the
+// first hit repeated) and the per-centroid distinct-neighbour count (out_cnt, optional: the
+// SA chain computes only those rows) are written per centroid row, coalesced.  Workgroups are
+// mapped so that all groups of a cloud run on one XCD (one L2 holds the cloud).
+//
+// Why this shape (profiles/r02_bq/): with lanes = points and one or a few centroids per wave
+// (round 1's design, and a multi-centroid LDS-tiled variant of it), every 64 point-centroid
+// pairs cost ~28 scalar instructions of ballot / popcount / exec bookkeeping: the SQ counters
+// showed 2x more SALU than VALU instructions, and SALU issue bounded the kernel (19-21 us at
+// SSG sa1).  Here the bookkeeping is per lane, ~9 vector instructions per point per 64
+// centroids and almost no scalar work (9 us).  Points by scalar loads instead of LDS
+// (uniform s_load_dwordx16, no staging) measured slower (11-13 us): SMEM returns out of order,
+// so every use waits for all loads in flight and their latency is exposed.
+#include <stdlib.h>
+
 #include "pn2_internal.h"
 
 namespace pn2 {
 
-template <int CP, int WPB>
-__global__ __launch_bounds__(64 * WPB) void ball_query_kernel(const float *__restrict__ pts,
-                                                              const float *__restrict__ ctr,
-                                                              int64_t B, int N, int S, int C,
-                                                              float r2, int K, int small,
-                                                              int64_t *__restrict__ out,
-                                                              int *__restrict__ out_cnt) {
+// CC > 0: the channel count is known at compile time (C = 3 xyz, C = 10 pose) and the shape is
+// not ATen's naive-bmm size; CC = 0: runtime C and the `small` flag.  NW bitmask words per
+// segment (TS = 32*NW points per wave per round).
+// one point record against one centroid: the reference's distance and masking test
+template <int CP>
+__device__ __forceinline__ unsigned bq_near(const float (&c)[CP], float ssq_c, const float *p, int C,
+                                            bool small, float r2) {
+    float mm = __fmul_rn(c[0], p[0]);
+#pragma unroll
+    for (int k = 1; k < CP - 1; ++k)
+        if (k < C) mm = small ? __fadd_rn(mm, __fmul_rn(c[k], p[k])) : __builtin_fmaf(c[k], p[k], mm);
+    float sp = p[CP - 1];
+#pragma unroll
+    for (int k = 1; k < CP - 1; ++k)
+        if (k == C) sp = p[k];  // static register indices (no scratch)
+    const float d = __fadd_rn(__fadd_rn(__fmul_rn(-2.0f, mm), ssq_c), sp);
+    return !(d > r2);
+}
+
+template <int CP, int CC, int NW, int P>
+__global__ __launch_bounds__(64 * P) void ball_query_kernel(
+    const float *__restrict__ pts, const float *__restrict__ ctr, int N, int S, int C_, float r2,
+    int K, int small_, int64_t *__restrict__ out, int *__restrict__ out_cnt) {
+    constexpr int TS = 32 * NW;
+    constexpr int TV = P * TS * CP / 4;  // float4 per staged round
+    __shared__ float4 tile[TV];
+    const int C = CC > 0 ? CC : C_;
+    const bool small = CC > 0 ? false : small_;  // the specialised instances never see tiny shapes
+    __shared__ int cnts[2][P][64];
+    __shared__ int firsts[64];
+
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t q = (int64_t)blockIdx.x * WPB + w;  // centroid (b*S + s)
-    if (q >= B * S) return;
-    const int64_t b = q / S;
+    const int gpc = (S + 63) >> 6;  // 64-centroid groups per cloud
+    int bid = blockIdx.x;
+    const int nb = gridDim.x;
+    if ((nb & 7) == 0) bid = (bid & 7) * (nb >> 3) + (bid >> 3);  // a cloud's groups on one XCD
+    const int b = bid / gpc;
+    const int g0 = (bid - b * gpc) * 64;
+    const int s = g0 + lane;
+    const bool valid = s < S;
+    const int64_t q = (int64_t)b * S + (valid ? s : g0);
 
-    // centroid record (wave-uniform)
-    float cq[CP];
-    const float4 *cptr = reinterpret_cast<const float4 *>(ctr + q * CP);
+    float c[CP];
+    {
+        const float4 *cp = reinterpret_cast<const float4 *>(ctr + q * CP);
 #pragma unroll
-    for (int v = 0; v < CP / 4; ++v) {
-        const float4 t = cptr[v];
-        cq[4 * v + 0] = t.x; cq[4 * v + 1] = t.y; cq[4 * v + 2] = t.z; cq[4 * v + 3] = t.w;
-    }
-    const float ssq_c = cq[C];
-
-    const float4 *P = reinterpret_cast<const float4 *>(pts + b * (int64_t)N * CP);
-    int64_t *o = out + q * K;
-    int cnt = 0;
-    int first = N;
-    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-
-    for (int n0 = 0; n0 < N; n0 += 64) {
-        const int n = n0 + lane;
-        bool hit = false;
-        if (n < N) {
-            float pp[CP];
-#pragma unroll
-            for (int v = 0; v < CP / 4; ++v) {
-                const float4 t = P[(int64_t)n * (CP / 4) + v];
-                pp[4 * v + 0] = t.x; pp[4 * v + 1] = t.y; pp[4 * v + 2] = t.z; pp[4 * v + 3] = t.w;
-            }
-            float mm = __fmul_rn(cq[0], pp[0]);
-            if (small) {
-#pragma unroll
-                for (int k = 1; k < CP - 1; ++k)
-                    if (k < C) mm = __fadd_rn(mm, __fmul_rn(cq[k], pp[k]));
-            } else {
-#pragma unroll
-                for (int k = 1; k < CP - 1; ++k)
-                    if (k < C) mm = __builtin_fmaf(cq[k], pp[k], mm);
-            }
-            const float d = __fadd_rn(__fadd_rn(__fmul_rn(-2.0f, mm), ssq_c), pp[C]);
-            hit = !(d > r2);
-        }
-        const unsigned long long m = __ballot(hit);
-        if (m) {
-            if (cnt == 0) first = n0 + (int)__builtin_ctzll(m);
-            const int pos = cnt + __builtin_popcountll(m & below);
-            if (hit && pos < K) o[pos] = n;
-            cnt += __builtin_popcountll(m);
-            if (cnt >= K) break;
+        for (int v = 0; v < CP / 4; ++v) {
+            const float4 t = cp[v];
+            c[4 * v + 0] = t.x; c[4 * v + 1] = t.y; c[4 * v + 2] = t.z; c[4 * v + 3] = t.w;
         }
     }
-    for (int k = cnt + lane; k < K; k += 64) o[k] = first;
-    // distinct neighbours: entries past them repeat entry 0 (the SA chain computes only these)
-    if (out_cnt && lane == 0) out_cnt[q] = min(cnt, K);
+    float ssq_c = c[CP - 1];
+#pragma unroll
+    for (int k = 1; k < CP - 1; ++k)
+        if (k == C) ssq_c = c[k];  // static register indices (no scratch)
+    if (w == 0) firsts[lane] = N;
+
+    int total = valid ? 0 : K;  // hits so far (invalid lanes count as done)
+    int r = 0;
+    for (int R0 = 0; R0 < N; R0 += P * TS, ++r) {
+        const int seg0 = R0 + w * TS;
+        unsigned bits[NW];
+        int mine = 0;
+        {  // stage the round's P*TS records (coalesced 16-byte loads by the whole workgroup)
+            if (R0 > 0) __syncthreads();  // every wave is done with the previous round's tile
+            const int nv = min(P * TS, N - R0) * (CP / 4);
+            const float4 *src = reinterpret_cast<const float4 *>(pts + ((int64_t)b * N + R0) * CP);
+            for (int x = threadIdx.x; x < nv; x += 64 * P) tile[x] = src[x];
+            __syncthreads();
+        }
+#pragma unroll
+        for (int t = 0; t < NW; ++t) {
+            const int base = seg0 + 32 * t;
+            const int np = min(32, N - base);  // points in this word (<= 0: none)
+            unsigned wd = 0;
+            if (np == 32) {
+#pragma unroll 8
+                for (int i = 0; i < 32; ++i) {
+                    const float4 *tp = tile + (w * TS + 32 * t + i) * (CP / 4);  // uniform address
+                    float pv[CP];
+#pragma unroll
+                    for (int v = 0; v < CP / 4; ++v) {
+                        const float4 q4 = tp[v];
+                        pv[4 * v] = q4.x; pv[4 * v + 1] = q4.y; pv[4 * v + 2] = q4.z; pv[4 * v + 3] = q4.w;
+                    }
+                    wd = (wd << 1) | bq_near<CP>(c, ssq_c, pv, C, small, r2);  // point base+i -> bit 31-i
+                }
+            } else if (np > 0) {
+                for (int i = 0; i < 32; ++i) {
+                    unsigned h = 0;
+                    if (i < np) {
+                        const float4 *tp = tile + (w * TS + 32 * t + i) * (CP / 4);
+                        float pv[CP];
+#pragma unroll
+                        for (int v = 0; v < CP / 4; ++v) {
+                            const float4 q4 = tp[v];
+                            pv[4 * v] = q4.x; pv[4 * v + 1] = q4.y; pv[4 * v + 2] = q4.z; pv[4 * v + 3] = q4.w;
+                        }
+                        h = bq_near<CP>(c, ssq_c, pv, C, small, r2);
+                    }
+                    wd = (wd << 1) | h;
+                }
+            }
+            bits[t] = wd;
+            mine += __builtin_popcount(wd);
+        }
+        cnts[r & 1][w][lane] = mine;
+        __syncthreads();
+        int off = total, round = 0;
+#pragma unroll
+        for (int v = 0; v < P; ++v) {
+            const int x = cnts[r & 1][v][lane];
+            if (v < w) off += x;
+            round += x;
+        }
+        // this segment's hits, in index order, into the slots [off, K)
+#pragma unroll
+        for (int t = 0; t < NW; ++t) {
+            unsigned wd = bits[t];
+            while (wd != 0 && off < K) {
+                const int i = __builtin_clz(wd);
+                const int n = seg0 + 32 * t + i;
+                if (off == 0) firsts[lane] = n;
+                out[q * K + off] = n;
+                ++off;
+                wd ^= 0x80000000u >> i;
+            }
+        }
+        total += round;
+        if (__builtin_amdgcn_ballot_w64(total < K) == 0) break;  // same in every wave
+    }
+    __syncthreads();  // firsts[] complete
+
+    // padding + counts, one centroid row per step (coalesced over the K slots)
+    for (int j = w; j < 64; j += P) {
+        if (g0 + j >= S) break;
+        const int cj = min(__builtin_amdgcn_readlane(total, j), K);
+        const int fj = firsts[j];
+        int64_t *o = out + ((int64_t)b * S + g0 + j) * K;
+        for (int k = cj + lane; k < K; k += 64) o[k] = fj;
+        if (out_cnt && lane == 0) out_cnt[(int64_t)b * S + g0 + j] = cj;
+    }
 }
 
 }  // namespace pn2
 
 using namespace pn2;
 
-template <int CP>
+template <int CP, int CC>
 static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, int64_t S,
                      int64_t C, float r2, int64_t K, int64_t *out, int *cnt, hipStream_t st) {
-    constexpr int WPB = 4;
-    const int64_t nq = B * S;
-    hipLaunchKernelGGL((ball_query_kernel<CP, WPB>), dim3((unsigned)((nq + WPB - 1) / WPB)),
-                       dim3(64 * WPB), 0, st, pp, cp_, B, (int)N, (int)S, (int)C, r2, (int)K,
-                       (int)(S * N * C < 400), out, cnt);
+    const int64_t nblk = B * ((S + 63) / 64);
+    PN2_REQUIRE(nblk < (int64_t)1 << 31, "pn2_ball_query_f32: too many centroids");
+    // waves per workgroup: 16 for long xyz clouds (more segments in flight), else 8
+    // (profiles/r02_bq/bq_modes.txt); PN2_BQ_WAVES=8|16 overrides (tuning)
+    int P = (CP == 4 && N >= 2048) ? 16 : 8;
+    if (const char *e = getenv("PN2_BQ_WAVES")) P = atoi(e) == 16 ? 16 : 8;
+    // words per segment: a round stages up to P*32*nw records (<= 64 per wave beyond xyz)
+    const int64_t per_wave = (N + P - 1) / P;
+    int nw = per_wave <= 32 ? 1 : per_wave <= 64 ? 2 : 4;
+    if (CP > 4 && nw > 2) nw = 2;
+    const int sm = (int)(S * N * C < 400);
+#define PN2_BQ_L(NW, PP)                                                                     \
+    hipLaunchKernelGGL((ball_query_kernel<CP, CC, NW, PP>), dim3((unsigned)nblk), dim3(64 * PP), \
+                       0, st, pp, cp_, (int)N, (int)S, (int)C, r2, (int)K, sm, out, cnt)
+    if (P == 8) {
+        if (nw == 1) PN2_BQ_L(1, 8);
+        else if (nw == 2) PN2_BQ_L(2, 8);
+        else PN2_BQ_L((CP > 4 ? 2 : 4), 8);
+    } else {
+        if (nw == 1) PN2_BQ_L(1, 16);
+        else if (nw == 2) PN2_BQ_L(2, 16);
+        else PN2_BQ_L((CP > 4 ? 2 : 4), 16);
+    }
+#undef PN2_BQ_L
     PN2_LAUNCH_CHECK("ball_query_kernel");
     return PN2_OK;
 }
@@ -112,16 +234,18 @@ extern "C" int pn2_ball_query_cnt_f32(const float *pts_packed, const float *ctr_
                 (long long)N, (long long)S, (long long)C, (long long)K);
     PN2_REQUIRE(K <= N, "pn2_ball_query_f32: sample_number %lld > N %lld", (long long)K,
                 (long long)N);
+    PN2_REQUIRE(N < (int64_t)1 << 30 && S < (int64_t)1 << 30, "pn2_ball_query_f32: N or S too large");
     if (B == 0 || S == 0) return PN2_OK;
     // radius ** 2 in double (Python float), compared in float32 like torch's wrapped scalar
     const float r2 = (float)(radius * radius);
     hipStream_t st = as_stream(stream);
     const int64_t cp = pn2_packed_stride(C);
-    if (cp == 4) return launch_bq<4>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
-    if (cp == 8) return launch_bq<8>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
-    if (cp == 12) return launch_bq<12>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
-    if (cp == 16) return launch_bq<16>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
-    if (cp == 20) return launch_bq<20>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
+#define PN2_BQ(CPV, CC) \
+    if (cp == CPV && (CC == 0 || (C == CC && S * N * C >= 400))) \
+        return launch_bq<CPV, CC>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
+    PN2_BQ(4, 3) PN2_BQ(12, 10)
+    PN2_BQ(4, 0) PN2_BQ(8, 0) PN2_BQ(12, 0) PN2_BQ(16, 0) PN2_BQ(20, 0)
+#undef PN2_BQ
     return set_error(PN2_EUNSUPPORTED, "pn2_ball_query_f32: C=%lld", (long long)C);
 }
 

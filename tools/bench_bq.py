@@ -1,0 +1,80 @@
+"""Time the ball query on the GPU for the BASELINE geometries.  Each shape is checked
+bit-exact against the CPU oracle on the first two clouds.  Prints one JSON line per shape:
+microseconds per launch (HIP events over 20 launches; run under rocprofv3 --kernel-trace for
+kernel-only times), pairs/s, and the fraction of the VALU and HBM peaks that represents."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "pointnet-like-pose-estimation_amd"), os.path.join(ROOT, "tests", "golden")):
+    sys.path.insert(0, p)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import cases  # noqa: E402
+import oracle  # noqa: E402
+import pn2  # noqa: E402,F401
+from pn2 import ops  # noqa: E402
+
+SHAPES = [  # (name, B, N, C, S, [(radius, K)], kind)
+    ("ssg_sa1", 32, 1024, 3, 512, [(0.2, 32)], "uniform3"),
+    ("ssg_sa2", 32, 512, 3, 128, [(0.4, 64)], "uniform3"),
+    ("msg_sa1", 32, 4096, 3, 512, [(0.1, 16), (0.2, 32), (0.4, 128)], "uniform3"),
+    ("pose_sa1", 64, 2048, 10, 512, [(0.2, 32)], "onehot10"),
+    ("stress_sa1", 128, 16384, 3, 512, [(0.2, 32)], "uniform3"),
+]
+VALU_PEAK = 256 * 4 * 32 * 2.4e9  # lane-ops/s: 256 CUs x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md)
+OPS_PER_PAIR = 9  # mul, 2 fma, add, sub, add, cmp, bit insert (+1/8 shift-or): the kernel's VALU
+HBM_PEAK = 8.0e12
+
+
+def main():
+    dev = torch.device("cuda")
+    res = []
+    for name, B, N, C, S, rks, kind in SHAPES:
+        x = cases.cloud(kind, B, N, 5)  # [B, N, C]
+        xd = x.to(dev)
+        start = torch.randint(0, N, (B,), generator=torch.Generator().manual_seed(1))
+        fidx, newp, cpk, ppk = ops.fps_direct(xd, S, start.to(dev))
+        for radius, K in rks:
+            want = oracle.query_ball_point(radius, K, x[:2], newp[:2].cpu())
+            ref, cnt = ops.ball_query_direct(ppk, cpk, C, radius, K, True)
+            for v in os.environ.get("BQ_MODES", "").split(","):  # PN2_BQ_MODE variants
+                if v:
+                    os.environ["PN2_BQ_MODE"] = v
+                else:
+                    os.environ.pop("PN2_BQ_MODE", None)
+                got = ops.ball_query_direct(ppk, cpk, C, radius, K)
+                # the count is the number of distinct entries before the padding starts
+                w = np.asarray(want)
+                wc = np.array([[min(K, int(np.argmax(np.r_[r[1:] == r[0], True])) + 1) if (r[1:] == r[0]).any() else K
+                                for r in bb] for bb in w])
+                ok = bool(np.array_equal(got[:2].cpu().numpy(), w)) and bool(torch.equal(got, ref))
+                cnt_ok = bool(np.array_equal(cnt[:2].cpu().numpy(), wc))
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                reps = 20
+                e0.record()
+                for _ in range(reps):
+                    ops.ball_query_direct(ppk, cpk, C, radius, K)
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / reps
+                pairs = float(B) * S * N
+                cp = ppk.shape[2]
+                nbytes = 4.0 * cp * B * (N + S) + 8.0 * B * S * K
+                r = {"shape": name, "radius": radius, "K": K, "mode": v or "default",
+                     "us": round(us, 2), "exact": ok, "count_exact": cnt_ok,
+                     "gpairs_per_s": round(pairs / us * 1e-3, 1),
+                     "valu_frac": round(OPS_PER_PAIR * pairs / (us * 1e-6) / VALU_PEAK, 4),
+                     "hbm_frac": round(nbytes / (us * 1e-6) / HBM_PEAK, 4)}
+                print(json.dumps(r), flush=True)
+                res.append(r)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "bq_sweep.json"), "w") as fh:
+        json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -22,8 +22,7 @@ for line in out.splitlines():
         cur = m.group(1)
         rows[cur] = {}
         continue
-    m = re.search(r"remark: (?:\S+ )?([A-Za-z ]+): (\d+)", line.split("]")[-1] if "]" in line else line)
-    m = re.search(r"\] ?([A-Za-z ]+?): (-?\d+)", line) or m
+    m = re.search(r"remark:\s+(.+?): (-?\d+) \[-Rpass", line)
     if cur and m:
         rows[cur][m.group(1).strip()] = int(m.group(2))
 for k, v in rows.items():
