@@ -85,8 +85,12 @@ def parse():
                     help="eager pipeline: run the head on its own stream (default off there)")
     ap.add_argument("--no-tail", action="store_true",
                     help="graphed pipeline: keep the head on the compute stream")
-    ap.add_argument("--slots", type=int, default=4,
-                    help="graphed pipeline: batches in flight (geometry runs slots-1 ahead)")
+    ap.add_argument("--slots", type=int, default=6,
+                    help="graphed pipeline: batch slots (a multiple of --geometry-batches; the "
+                         "geometry runs slots/geometry-batches - 1 groups ahead)")
+    ap.add_argument("--geometry-batches", type=int, default=2,
+                    help="graphed pipeline: consecutive batches whose geometry (FPS + ball "
+                         "queries) runs as one replay over their clouds side by side")
     ap.add_argument("--geometry-streams", type=int, default=2,
                     help="graphed pipeline: 2 = consecutive batches' FPS chains on two streams")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -322,7 +326,8 @@ def main():
         if not a.eager_pipeline:
             pf = GraphedPipeline(pmodel, geometry_cus=a.geometry_cus,
                                  tail=not a.no_tail, nslots=a.slots,
-                                 geometry_streams=a.geometry_streams)
+                                 geometry_streams=a.geometry_streams,
+                                 geometry_batches=a.geometry_batches)
         else:
             pf = PipelinedForward(pmodel, geometry_cus=a.geometry_cus,
                                   tail="auto" if a.tail else False)
@@ -429,7 +434,9 @@ def main():
                            " + head" if (not a.eager_pipeline and not a.no_tail) or (
                                a.tail and not names[0].startswith("translation")) else "",
                            " on %d dedicated CUs" % a.geometry_cus if a.geometry_cus > 0
-                           else "s sharing all CUs")
+                           else "s sharing all CUs") + (
+                           "; geometry of %d batches per replay" % a.geometry_batches
+                           if not a.eager_pipeline else "")
                        if pipelined else "eager"),
             "eager_value": round(eager_value, 2),
         }

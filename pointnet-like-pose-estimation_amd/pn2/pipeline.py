@@ -316,7 +316,26 @@ _MODE = "thread_local"
 
 
 class _Slot:
-    """Static buffers and graphs of one pipeline slot (batches i with i % nslots == slot)."""
+    """Static buffers and graphs of one batch slot: one batch of a geometry group."""
+
+
+class _Group:
+    """Static inputs and the geometry graph of ``geometry_batches`` consecutive batches; its
+    ``halves`` are their batch slots."""
+
+
+def _batched_like(x, n):
+    """An uninitialised [n * B, ...] tensor whose every [B, ...] slice has x's strides (so a
+    cloud keeps its memory layout, on which the reference's summation orders depend), or None
+    when the batch is not x's outermost dimension."""
+    order = sorted(range(x.dim()), key=lambda d: (-x.stride(d), d))
+    if order[0] != 0:
+        return None
+    shape = [x.shape[d] for d in order]
+    shape[0] *= n
+    buf = torch.empty(shape, dtype=x.dtype, device=x.device)
+    inv = [order.index(d) for d in range(x.dim())]
+    return buf.permute(inv)
 
 
 class GraphedPipeline(PipelinedForward):
@@ -324,47 +343,56 @@ class GraphedPipeline(PipelinedForward):
 
     The eager pipeline issues ~25 launches plus the SA modules' Python per batch; on MI355X that
     host time (~0.5 ms per SSG B=32 batch) is as long as the GPU work, so the GPU idles.  Here
-    each of ``nslots`` slots (batch i uses slot i % nslots) holds static inputs and three
-    captured graphs:
-      fps   the batch's geometry (``_fps_chain``: FPS + ball queries), replayed on the geometry
-            stream ``nslots - 1`` batches ahead of the compute stream;
-      sa    the forward up to the last SA layer, replayed on the compute stream;
-      head  the rest of the forward, replayed on a third stream with the geometry CUs (``tail``;
-            with tail=False, head is part of sa).
-    The capture is split by a forward hook (capture_end / capture_begin) after the last SA layer
-    that groups neighbourhoods (``_split_index``: a trailing group_all layer goes with the head;
-    the eager ``PipelinedForward`` tail still splits after the last SA layer).
-    Events order the slot reuse: batch i+nslots's fps waits until batch i's sa and head graphs
-    and the output clone have run (it overwrites the slot's inputs and geometry outputs, which
-    a group_all layer in the head graph still reads), batch i+nslots's sa waits for batch i's
-    head (they share a memory pool).  A slot's fps -> sa -> head is thus a dependency cycle that
-    nslots batches must cover: 4 slots (default) measured 84.5-84.9k clouds/s at SSG against
-    74-77k with 3 (5 and 6 within noise of 4).  Static memory makes the tail safe for every
-    head here, including the translation heads' ``mean`` (see PipelinedForward).
+    batches are taken in *groups* of ``geometry_batches`` consecutive batches; each of the
+    ``nslots // geometry_batches`` group slots (group g uses slot g % groups) holds static
+    inputs for its batches and one captured geometry graph, and each of its batch slots two
+    forward graphs:
+      fps   the group's geometry (``_fps_chain`` over the group's batches side by side: FPS +
+            ball queries), replayed on a geometry stream ``groups - 1`` groups ahead of the
+            compute stream;
+      sa    a batch's forward up to the last SA layer, replayed on the compute stream;
+      head  the rest of the forward, replayed on a third stream (``tail``; with tail=False,
+            head is part of sa).
+    Each batch's forward reads its own slice of the group's geometry, so it computes exactly
+    what its own eager forward computes (per-cloud kernels; the FC tail's row kernel computes a
+    row the same way at any row count).  The capture is split by a forward hook
+    (capture_end / capture_begin) after the last SA layer that groups neighbourhoods
+    (``_split_index``: a trailing group_all layer goes with the head; the eager
+    ``PipelinedForward`` tail still splits after the last SA layer).
+
+    Why groups: FPS is a serial, latency-bound loop on one workgroup per cloud, so a launch
+    over 2B clouds takes about what one over B clouds takes.  Under the MLP kernels' contention
+    one SSG B=32 batch's FPS chain took 690-770 us (tools/debug/gpipe_events.py) against a
+    ~300 us compute period: with one batch per geometry replay and two geometry streams the
+    pipeline was geometry-bound at ~375 us per batch.  Two batches per replay halve that.
+
+    Events order the slot reuse: group g+groups's fps waits until group g's batches' sa and head
+    graphs and output clones have run (it overwrites the group's inputs and geometry outputs,
+    which a group_all layer in a head graph still reads); a batch's sa waits for the head of
+    the batch that used its batch slot before (they share a memory pool).
 
     RNG and results: as PipelinedForward.  The first batch of a new input signature (or after
     any parameter change) runs through the eager pipeline -- its real result, its draws -- and
     every slot is captured after it; the captures draw nothing.  Every replayed batch takes its
-    draws on the host in batch order (shard.draw_start, so shard.batch_shard applies) and uploads
-    them into the slot before its fps replay.  Outputs are cloned out of the static buffers on
-    the stream that produced them, so they stay valid.
+    draws on the host in batch order (shard.draw_start, so shard.batch_shard applies) into its
+    part of the group's start buffer, uploaded before the group's fps replay.  A last group
+    with fewer batches repeats its first batch's input in the empty places (no draws, results
+    unused).  Outputs are cloned out of the static buffers on the stream that produced them.
 
-    geometry_streams=2 (default, shared CUs): consecutive batches' geometry replays alternate
-    between two high-priority streams.  The FPS chain is latency-bound on 32 workgroups (one per
-    cloud) and, under contention with the MLP kernels, took ~377 us per SSG batch against the
-    compute stream's ~350 us -- the pipeline was geometry-bound (tools/debug/gpipe_events.py).
-    Two batches' chains in flight halve the geometry period; the compute stream is now the bound.
-
-    Measured (SSG B=32 N=1024, shared CUs): one geometry stream 72k-74k clouds/s, two 76.4k-77.7k
-    (against 52.5k-67.6k for the eager pipeline: host-bound, ~470 us of issue per batch vs ~210
-    us here, tools/debug/host_cost.py).  Without the tail the head's dozen launches sit on the
-    compute stream (59.5k).
+    geometry_streams=2 (default, shared CUs): consecutive groups' geometry replays alternate
+    between two high-priority streams.  More streams exceed the 4 hardware queues a process
+    gets (GPU_MAX_HW_QUEUES) with the compute and tail streams.
     """
 
-    def __init__(self, model, geometry_cus=0, tail=True, nslots=4, geometry_streams=2):
+    def __init__(self, model, geometry_cus=0, tail=True, nslots=6, geometry_streams=2,
+                 geometry_batches=2):
         super().__init__(model, geometry_cus, bool(tail))
-        if nslots < 2:
-            raise ValueError("pn2.pipeline: GraphedPipeline needs at least 2 slots")
+        gb = int(geometry_batches)
+        if gb < 1:
+            raise ValueError("pn2.pipeline: geometry_batches must be >= 1")
+        if nslots < 2 * gb or nslots % gb:
+            raise ValueError("pn2.pipeline: GraphedPipeline needs nslots a multiple of "
+                             "geometry_batches and at least two groups")
         if geometry_cus > 0:
             geometry_streams = 1  # the CU-partitioned geometry stream is one
         # 2 at most: with the compute and tail streams that is the 4 hardware queues a process
@@ -373,10 +401,12 @@ class GraphedPipeline(PipelinedForward):
         if geometry_streams not in (1, 2):
             raise ValueError("pn2.pipeline: geometry_streams is 1 or 2")
         self.nslots = int(nslots)
+        self.gb = gb
+        self.ngroups = self.nslots // gb
         self.geometry_streams = int(geometry_streams)
         self.trace = None
         self._key = None
-        self._slots = None
+        self._slots = None  # the group slots
 
     def _state_key(self, x, extra):
         from .graphs import _sig
@@ -394,7 +424,7 @@ class GraphedPipeline(PipelinedForward):
         would compete with FPS on a few CUs.  PN2_PIPE_SPLIT=last keeps the old split (A/B).
 
         The head graph then reads the split layer's outputs -- sa2's centroids are a static
-        output of the slot's fps graph -- so the slot's next fps replay waits for the head
+        output of the group's fps graph -- so the group's next fps replay waits for the head
         (``ev_read`` in ``run``), not only for the sa graph."""
         k = len(self.sas) - 1
         if (k > 0 and getattr(self.sas[k], "group_all", False) and self.geometry_cus <= 0 and
@@ -403,29 +433,72 @@ class GraphedPipeline(PipelinedForward):
         return k
 
     def _capture(self, x, extra, dev, draws):
-        sl = _Slot()
-        sl.x = x.clone()
-        sl.extra = tuple(e.clone() for e in extra)
-        # the start slots exist before the capture: allocated inside it, a slot could share
-        # pool memory with a temporary the capture freed earlier, which the replay rewrites
-        # after the slot was uploaded
-        # all of a batch's start draws in one device buffer: one upload per batch
-        sl.start_buf = torch.empty(sum(B for B, _ in draws), dtype=torch.long, device=dev)
-        sl.starts, off = [], 0
-        for B, N in draws:
-            sl.starts.append((sl.start_buf[off:off + B], B, N))
-            off += B
-        it = iter(sl.starts)
+        gb, B = self.gb, x.shape[0]
+        grp = _Group()
+        grp.x = _batched_like(x, gb) if gb > 1 else None
+        if grp.x is None:
+            if gb > 1:
+                raise RuntimeError("pn2.pipeline: geometry_batches > 1 needs the batch as the "
+                                   "input's outermost dimension")
+            grp.x = x.clone()
+        grp.x.copy_(torch.cat([x] * gb) if gb > 1 else x)
+        xs = [grp.x[h * B:(h + 1) * B] for h in range(gb)]
+        # the start buffer exists before the capture: allocated inside it, it could share pool
+        # memory with a temporary the capture freed earlier, which the replay rewrites after
+        # the buffer was uploaded.  Layout: per draw d of a batch (layer order), a block of
+        # gb * B_d starts, batch h of the group at [h * B_d, (h + 1) * B_d) of the block.
+        grp.start_buf = torch.empty(gb * sum(b for b, _ in draws), dtype=torch.long, device=dev)
+        blocks, off = [], 0
+        for b, n in draws:
+            blocks.append((grp.start_buf[off:off + gb * b], gb * b, n))
+            off += gb * b
+        it = iter(blocks)
 
-        def static_start(B, N, device):
+        def static_start(Bq, Nq, device):
             t, b, n = next(it)
-            if (b, n) != (B, N):
+            if (b, n) != (Bq, Nq):
                 raise RuntimeError("pn2.pipeline: FPS draw shapes changed during capture")
             return t
 
-        sl.fps, sl.sa = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        grp.fps = torch.cuda.CUDAGraph()
+        fps_pool = torch.cuda.graph_pool_handle()
+        cs = torch.cuda.Stream(dev)
+        torch.cuda.synchronize(dev)
+        with torch.no_grad(), torch.cuda.stream(cs), shard.start_source(static_start):
+            grp.fps.capture_begin(pool=fps_pool, capture_error_mode=_MODE)
+            entries = self._fps_chain(grp.x)
+            grp.fps.capture_end()
+        torch.cuda.synchronize(dev)
+        # each batch's slice of the group's geometry, keyed by the tensor its SA module is
+        # called with in that batch's forward (its slice of the input or of the previous
+        # layer's centroids)
+        srcs = {grp.x.data_ptr(): grp.x}
+        for _, newp, _, _, _ in entries.values():
+            srcs[newp.data_ptr()] = newp
+
+        def part(t, h):
+            return t[h * B:(h + 1) * B]
+
+        geo = set()
+        for _, newp, cpk, ppk, idxs in entries.values():
+            geo.update(t.untyped_storage().data_ptr()
+                       for t in [newp, cpk, ppk] + [t for ic in idxs for t in ic])
+        grp.halves = []
+        for h in range(gb):
+            ent = {k: (part(srcs[ptr], h).data_ptr(), part(newp, h), part(cpk, h), part(ppk, h),
+                       [tuple(part(t, h) for t in ic) for ic in idxs])
+                   for k, (ptr, newp, cpk, ppk, idxs) in entries.items()}
+            grp.halves.append(self._capture_forward(xs[h], extra, dev, ent, geo))
+        grp.entries = entries
+        return grp
+
+    def _capture_forward(self, x, extra, dev, entries, geo):
+        sl = _Slot()
+        sl.x = x
+        sl.extra = tuple(e.clone() for e in extra)
+        sl.sa = torch.cuda.CUDAGraph()
         sl.head = torch.cuda.CUDAGraph() if self.tail else None
-        fps_pool, fwd_pool = torch.cuda.graph_pool_handle(), torch.cuda.graph_pool_handle()
+        fwd_pool = torch.cuda.graph_pool_handle()
 
         def split(module, inputs, output):
             sl.sa.capture_end()
@@ -437,25 +510,17 @@ class GraphedPipeline(PipelinedForward):
         handle = self.sas[self._split_index()].register_forward_hook(split) if self.tail else None
         try:
             with torch.no_grad(), torch.cuda.stream(cs):
-                with shard.start_source(static_start):
-                    sl.fps.capture_begin(pool=fps_pool, capture_error_mode=_MODE)
-                    sl.entries = self._fps_chain(sl.x)
-                    sl.fps.capture_end()
                 sl.sa.capture_begin(pool=fwd_pool, capture_error_mode=_MODE)
-                with geometry.provide(dict(sl.entries)):
+                with geometry.provide(dict(entries)):
                     sl.out = self.model(sl.x, *sl.extra)
                 (sl.head if self.tail else sl.sa).capture_end()
         finally:
             if handle is not None:
                 handle.remove()
         torch.cuda.synchronize(dev)
-        # does anything after the sa graph read the fps graph's outputs?  The head graph does
-        # when it holds a layer (a trailing group_all reads the split layer's centroids); the
-        # output clone does when the model returns one of them
-        geo = set()
-        for _, newp, cpk, ppk, idxs in sl.entries.values():
-            geo.update(t.untyped_storage().data_ptr()
-                       for t in [newp, cpk, ppk] + [t for ic in idxs for t in ic])
+        # does anything after the sa graph read the geometry graph's outputs?  The head graph
+        # does when it holds a layer (a trailing group_all reads the split layer's centroids);
+        # the output clone does when the model returns one of them
         outs = sl.out if isinstance(sl.out, (tuple, list)) else (sl.out,)
         flat = [t for o in outs for t in (o if isinstance(o, (tuple, list)) else (o,))]
         sl.tail_reads_geometry = (self.tail and self._split_index() < len(self.sas) - 1) or any(
@@ -484,21 +549,24 @@ class GraphedPipeline(PipelinedForward):
             with shard.start_source(record):
                 outs = self._run_eager(batches[:1], None if extras is None else extras[:1],
                                        post, False)
+            self._draws = draws
             self._slots = [self._capture(batches[0], extra_of(0), dev, draws)
-                           for _ in range(self.nslots)]
+                           for _ in range(self.ngroups)]
             self._key = self._state_key(batches[0], extra_of(0))
             first = 1
         if first == len(batches):
             return outs
+        gb, ng = self.gb, self.ngroups
+        nbat = len(batches) - first
+        ngr = (nbat + gb - 1) // gb  # groups this call
         geo, main, tail = _streams(dev.index, self.geometry_cus)
         geos = [geo] + _extra_geometry_streams(dev.index, self.geometry_streams - 1)
         caller = torch.cuda.current_stream(dev)
         for st in geos + [main, tail]:
             st.wait_stream(caller)
-        ns = self.nslots
-        ev_fps, ev_sa, ev_head = [None] * ns, [None] * ns, [None] * ns
-        ev_read = [None] * ns  # last read of a slot's fps outputs (sa, or head + clone)
-        starts = self._draw_all(len(batches) - first)
+        ev_fps, ev_read = [None] * ng, [None] * ng  # per group slot
+        ev_head = [None] * (ng * gb)  # per batch slot
+        starts = self._draw_all(ngr)
 
         tr = self.trace  # optional list of per-batch timing events (tools/debug/gpipe_events.py)
 
@@ -510,56 +578,63 @@ class GraphedPipeline(PipelinedForward):
                 e.record(stream)
                 tr[j][name] = (e, time.perf_counter())
 
-        def issue_fps(j):
-            s = j % ns
-            sl = self._slots[s]
-            geo = geos[j % len(geos)]
+        def issue_fps(g):
+            s = g % ng
+            grp = self._slots[s]
+            geo = geos[g % len(geos)]
+            js = [first + g * gb + h for h in range(gb)]
+            nh = sum(1 for j in js if j < len(batches))
             with torch.cuda.stream(geo):
-                # batch j-ns is done with the slot's inputs and geometry outputs: its sa graph
-                # read them, and so did its head graph when the split put a group_all layer
-                # there (sa3 reads sa2's centroids, a static output of the fps graph)
+                # the group slot's previous batches are done with its inputs and geometry
+                # outputs: their sa graphs read them, and so did their head graphs when the
+                # split put a group_all layer there (sa3 reads sa2's centroids)
                 if ev_read[s] is not None:
                     geo.wait_event(ev_read[s])
-                mark(j, "geo0", geo)
-                sl.x.copy_(batches[j], non_blocking=True)
-                sl.start_buf.copy_(self._draw_row(starts, j - first), non_blocking=True)
-                sl.fps.replay()
+                mark(js[0] - first, "geo0", geo)
+                for h, j in enumerate(js):
+                    grp.halves[h].x.copy_(batches[j if j < len(batches) else js[0]],
+                                          non_blocking=True)
+                grp.start_buf.copy_(self._draw_row(starts, g, nh), non_blocking=True)
+                grp.fps.replay()
                 ev_fps[s] = geo.record_event()
-                mark(j, "geo1", geo)
+                mark(js[0] - first, "geo1", geo)
 
         with torch.no_grad():
-            # the geometry runs ns-1 batches ahead of the compute stream
-            for j in range(first, min(first + ns - 1, len(batches))):
-                issue_fps(j)
+            # the geometry runs ng-1 groups ahead of the compute stream
+            for g in range(min(ng - 1, ngr)):
+                issue_fps(g)
             for i in range(first, len(batches)):
-                s = i % ns
-                sl = self._slots[s]
-                if i + ns - 1 < len(batches):
-                    issue_fps(i + ns - 1)
+                g, h = divmod(i - first, gb)
+                s = g % ng
+                bs = s * gb + h
+                sl = self._slots[s].halves[h]
+                if h == 0 and g + ng - 1 < ngr:
+                    issue_fps(g + ng - 1)
                 with torch.cuda.stream(main):
                     main.wait_event(ev_fps[s])
-                    if ev_head[s] is not None:  # batch i-ns's head is done with the pool
-                        main.wait_event(ev_head[s])
+                    if ev_head[bs] is not None:  # the batch slot's last head is done with the pool
+                        main.wait_event(ev_head[bs])
                     for d, e in zip(sl.extra, extra_of(i)):
                         d.copy_(e, non_blocking=True)
-                    mark(i, "sa0", main)
+                    mark(i - first, "sa0", main)
                     sl.sa.replay()
-                    ev_sa[s] = main.record_event()
-                    mark(i, "sa1", main)
+                    ev_sa = main.record_event()
+                    mark(i - first, "sa1", main)
                 ts = tail if sl.head is not None else main
                 with torch.cuda.stream(ts):
                     if sl.head is not None:
-                        ts.wait_event(ev_sa[s])
-                        mark(i, "hd0", ts)
+                        ts.wait_event(ev_sa)
+                        mark(i - first, "hd0", ts)
                         sl.head.replay()
                     out = _clone(sl.out)
-                    # recorded before `post` (e.g. an all_gather) so the next fps replay of
-                    # this slot does not wait for the collective
-                    ev_read[s] = ts.record_event() if sl.tail_reads_geometry else ev_sa[s]
+                    # recorded before `post` (e.g. an all_gather) so the group's next fps
+                    # replay does not wait for the collective; a later batch of the group
+                    # replaces it (same streams, later in their order)
+                    ev_read[s] = ts.record_event() if sl.tail_reads_geometry else ev_sa
                     if post is not None:
                         out = post(i, out)
-                    ev_head[s] = ts.record_event()
-                    mark(i, "hd1", ts)
+                    ev_head[bs] = ts.record_event()
+                    mark(i - first, "hd1", ts)
                 outs.append(out)
         for g in geos[1:]:
             geo.wait_stream(g)
@@ -569,15 +644,14 @@ class GraphedPipeline(PipelinedForward):
         return outs
 
     def _draw_all(self, k):
-        """The pinned host buffer that receives the start draws of the next k batches, one row
-        per batch (one asynchronous upload per batch, no per-draw pinning on the issue path).
-        Rows are drawn by ``_draw_row`` just before their batch's upload is issued -- in batch
-        order then layer order, the order k eager forwards take them -- so the host draws
-        overlap the GPU work of earlier batches instead of delaying the first launch.  Two
+        """The pinned host buffer that receives the start draws of the next k groups, one row
+        per group (one asynchronous upload per group, no per-draw pinning on the issue path).
+        Rows are drawn by ``_draw_row`` just before their group's upload is issued -- batch by
+        batch, each in layer order: the order k eager forwards take them -- so the host draws
+        overlap the GPU work of earlier groups instead of delaying the first launch.  Two
         buffers alternate across calls; one is reused once the uploads of the call before last
         ran."""
-        shapes = [(B, N) for _, B, N in self._slots[0].starts]
-        width = sum(B for B, _ in shapes)
+        width = self.gb * sum(B for B, _ in self._draws)
         if not hasattr(self, "_pinned"):
             self._pinned, self._pinned_evs, self._pinned_cur = [None, None], [None, None], 0
         c = self._pinned_cur = 1 - self._pinned_cur
@@ -587,12 +661,19 @@ class GraphedPipeline(PipelinedForward):
         if buf is None or buf.shape[0] < k or buf.shape[1] != width:
             buf = self._pinned[c] = torch.empty(max(k, 64), width, dtype=torch.long,
                                                 pin_memory=True)
-        self._shapes = shapes
         return buf
 
-    def _draw_row(self, buf, j):
-        off = 0
-        for B, N in self._shapes:
-            buf[j, off:off + B] = shard.draw_start(B, N, pin=False)
-            off += B
-        return buf[j]
+    def _draw_row(self, buf, g, nh):
+        """Group g's starts: batches 0..nh-1 of the group draw (in batch, then layer order) into
+        their places of the start layout (see _capture); the empty places get 0."""
+        gb = self.gb
+        for h in range(gb):
+            off = 0
+            for B, N in self._draws:
+                dst = buf[g, off + h * B:off + (h + 1) * B]
+                if h < nh:
+                    dst.copy_(shard.draw_start(B, N, pin=False))
+                else:
+                    dst.zero_()
+                off += gb * B
+        return buf[g]

@@ -26,8 +26,9 @@ else:
 cases.randomize_bn(model, 8)
 model = model.to(DEV)
 x = cases.cloud(kind, B, N, 90).permute(0, 2, 1).contiguous().to(DEV)
-gp = GraphedPipeline(model, nslots=int(os.environ.get("SLOTS", "3")),
-                     geometry_streams=int(os.environ.get("GEOS", "1")))
+gp = GraphedPipeline(model, nslots=int(os.environ.get("SLOTS", "6")),
+                     geometry_streams=int(os.environ.get("GEOS", "2")),
+                     geometry_batches=int(os.environ.get("GB", "2")))
 ex = [(torch.zeros(B, 3, device=DEV),)] if os.environ.get("CONFIG", "ssg") == "pose" else None
 gp.run([x] * 3, None if ex is None else ex * 3)
 torch.cuda.synchronize()
@@ -44,7 +45,8 @@ for i, m in enumerate(tr):
     h = {k: (m[k][1] - h0) * 1e6 for k in names if k in m}
     print("%3d  " % i + " ".join("%8.1f" % g.get(k, float("nan")) for k in names) + "  | " +
           " ".join("%8.1f" % h.get(k, float("nan")) for k in ("geo0", "sa0", "hd0")) +
-          "   %5.1f %5.1f %5.1f" % (g["geo1"] - g["geo0"], g["sa1"] - g["sa0"], g["hd1"] - g["hd0"]))
+          "   %5.1f %5.1f %5.1f" % (g.get("geo1", float("nan")) - g.get("geo0", float("nan")),
+                                   g["sa1"] - g["sa0"], g["hd1"] - g["hd0"]))
 per = [(e0.elapsed_time(tr[i + 1]["sa0"][0]) - e0.elapsed_time(tr[i]["sa0"][0])) * 1e3
        for i in range(len(tr) - 1)]
 print("period sa0->sa0: median %.1f us" % sorted(per)[len(per) // 2])

@@ -32,8 +32,9 @@ cases.randomize_bn(model, 8)
 model = model.to(DEV)
 x = cases.cloud(kind, B, N, 90).permute(0, 2, 1).contiguous().to(DEV)
 ex = [(torch.zeros(B, 3, device=DEV),)] if pose else None
-gp = GraphedPipeline(model, nslots=int(os.environ.get("SLOTS", "4")),
-                     geometry_streams=int(os.environ.get("GEOS", "2")))
+gp = GraphedPipeline(model, nslots=int(os.environ.get("SLOTS", "6")),
+                     geometry_streams=int(os.environ.get("GEOS", "2")),
+                     geometry_batches=int(os.environ.get("GB", "2")))
 K = 100
 gp.run([x] * 3, None if ex is None else ex * 3)
 torch.cuda.synchronize()
@@ -52,15 +53,17 @@ def rate():
 
 print("full     %.0f clouds/s" % rate())
 for stage in ("fps", "sa", "head"):
-    saved = [getattr(sl, stage) for sl in gp._slots]
+    # fps graphs belong to the group slots, sa / head graphs to their batch slots
+    objs = list(gp._slots) if stage == "fps" else [h for grp in gp._slots for h in grp.halves]
+    saved = [getattr(o, stage) for o in objs]
     if saved[0] is None:
         continue
 
     class Nop:
         def replay(self):
             pass
-    for sl in gp._slots:
-        setattr(sl, stage, Nop())
+    for o in objs:
+        setattr(o, stage, Nop())
     print("no_%-5s %.0f clouds/s" % (stage, rate()))
-    for sl, g in zip(gp._slots, saved):
-        setattr(sl, stage, g)
+    for o, g in zip(objs, saved):
+        setattr(o, stage, g)
