@@ -9,19 +9,21 @@
 // practice the launch: the library GEMMs chosen for these shapes run 5-13 us each, several
 // times the weight's read time.
 //
-// Layout: one wave per kLinRows (4 or 2 by the row count) consecutive output features; each
-// lane walks K with 16-byte loads of the W rows (coalesced: a wave reads 1 KB of a row per step) and of the x rows (L2
-// resident: x is at most 16 x K floats), accumulating kLinRows x B partial dot products in
-// registers, then a transpose-reduce across the wave (32 shuffles for the 32 sums).  Float32
-// FMA throughout (the library GEMM's arithmetic; the summation order differs, as between any
-// two GEMM kernels).  Measured per call in a graph (tools/debug/fc_shapes.py), B = 8:
-// 1024->512 5.8 us (library + ReLU 7.6), 512->256 4.3 (12.7), 256->9 3.1 (4.8), 256->4096 3.8
-// (5.9).  More rows run as blocks of 16 (grid.y).
+// Layout: one workgroup of 4 waves per kLinRows (4 or 2 by the row count) consecutive output
+// features; the four waves split K (256-float chunk c goes to wave c % 4), each lane walking its
+// chunks with 16-byte loads of the W rows (coalesced: a wave reads 1 KB of a row per chunk) and
+// of the x rows (L2 resident: x is at most 16 x K floats), accumulating kLinRows x B partial
+// dot products in registers; then a transpose-reduce across each wave (32 shuffles for the 32
+// sums) and the four waves' sums added in LDS in wave order.  With K split over the waves
+// every load of a layer is in flight at once (one wave walking all of K waited for its loads
+// chunk by chunk: 9.8 us for 1024->512 at B=32, latency-bound).  Float32 FMA throughout (the
+// library GEMM's arithmetic; the summation order differs, as between any two GEMM kernels).
+// More rows run as blocks of 16 (grid.y).
 #include "pn2_internal.h"
 
 namespace pn2 {
 
-constexpr int kLinWaves = 4;   // waves per workgroup
+constexpr int kLinWaves = 4;   // waves per workgroup (they split K)
 
 // output features per wave: kLinRows x BT accumulators stay within ~128 VGPRs
 template <int BT>
@@ -55,8 +57,8 @@ __global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float
     x += (int64_t)blockIdx.y * BT * ldx;
     out += (int64_t)blockIdx.y * BT * ldo;
     B = B - (int)blockIdx.y * BT < BT ? B - (int)blockIdx.y * BT : BT;
-    const int64_t o0 = ((int64_t)blockIdx.x * kLinWaves + threadIdx.x / 64) * kLinRows;
-    if (o0 >= N) return;  // whole waves leave together
+    const int wave = threadIdx.x / 64;
+    const int64_t o0 = (int64_t)blockIdx.x * kLinRows;
     float acc[kLinRows][BT];
 #pragma unroll
     for (int r = 0; r < kLinRows; ++r)
@@ -72,7 +74,7 @@ __global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float
 #pragma unroll
     for (int b = 0; b < BT; ++b) xr[b] = x + (int64_t)(b < B ? b : B - 1) * ldx;
     if (vec) {  // 16-byte aligned rows (host-checked)
-        for (int64_t k = (int64_t)lane * 4; k < K; k += 256) {
+        for (int64_t k = (int64_t)wave * 256 + lane * 4; k < K; k += 256 * kLinWaves) {
             float4 w[kLinRows], v[BT];
 #pragma unroll
             for (int r = 0; r < kLinRows; ++r) w[r] = *reinterpret_cast<const float4 *>(wr[r] + k);
@@ -92,7 +94,7 @@ __global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float
             }
         }
     } else {
-        for (int64_t k = lane; k < K; k += 64) {
+        for (int64_t k = (int64_t)wave * 64 + lane; k < K; k += 64 * kLinWaves) {
             float w[kLinRows], v[BT];
 #pragma unroll
             for (int r = 0; r < kLinRows; ++r) w[r] = wr[r][k];
@@ -120,8 +122,15 @@ __global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float
     lin_reduce_step<1>(a, lane);
     a[0] += __shfl_xor(a[0], 1);
     const int v = (lane >> 1) & 31, r = v / BT, b = v % BT;
-    if ((lane & 1) == 0 && b < B && o0 + r < N) {
-        const float y = a[0] + (bias ? bias[o0 + r] : 0.f);
+    // the waves' sums, added in wave order (the same order for every row count)
+    __shared__ float red[kLinWaves][32];
+    if ((lane & 1) == 0) red[wave][v] = a[0];
+    __syncthreads();
+    if (wave == 0 && (lane & 1) == 0 && b < B && o0 + r < N) {
+        float y = red[0][v];
+#pragma unroll
+        for (int w = 1; w < kLinWaves; ++w) y += red[w][v];
+        y += bias ? bias[o0 + r] : 0.f;
         out[b * ldo + o0 + r] = relu ? (y > 0.f ? y : 0.f) : y;
     }
 }
@@ -143,8 +152,7 @@ extern "C" int pn2_linear_rows_f32(const float *x, int64_t ldx, int64_t B, int64
     const int relu = (flags & PN2_LINEAR_RELU) ? 1 : 0;
     hipStream_t st = as_stream(stream);
     auto grid = [N, B](int rows, int bt) {
-        const int64_t waves = (N + rows - 1) / rows;
-        return dim3((unsigned)((waves + kLinWaves - 1) / kLinWaves), (unsigned)((B + bt - 1) / bt));
+        return dim3((unsigned)((N + rows - 1) / rows), (unsigned)((B + bt - 1) / bt));
     };
     const dim3 block(64 * kLinWaves);
     if (B <= 8)

@@ -134,6 +134,13 @@ __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
     return ~wave_max_u32(~v);
 }
 
+// Logical workgroup id under which every XCD runs a contiguous range of ids (dispatch places
+// workgroup i on XCD i % 8, each XCD with its own L2): consecutive logical ids -- a cloud's
+// row blocks, or the groups of one cloud -- share an L2.  Identity unless n % 8 == 0.
+__device__ __forceinline__ unsigned xcd_contiguous(unsigned id, unsigned n) {
+    return (n & 7u) ? id : (id & 7u) * (n >> 3) + (id >> 3);
+}
+
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 }  // namespace pn2

@@ -190,7 +190,10 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     const int lane = tid & 63;
     const int r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int slab = blockIdx.x * kChainWaves + wave;
+    // a cloud's workgroups on one XCD: its rows gather the same points (and the pre-pass wrote
+    // that cloud's z rows from the same XCD, see sa_dense.hip)
+    const int bid = (int)xcd_contiguous(blockIdx.x, gridDim.x);
+    const int slab = bid * kChainWaves + wave;
     const pn2_sa_src &s = A.src;
     const ChainLayer &L0 = A.L[0], &L1 = A.L[1], &L2 = A.L[2];
     const int coutL = 32 * L2.tiles;
@@ -198,9 +201,9 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     unsigned c_g0 = 0;
     int c_ng = 0, c_flags = 0;
     if (compact) {
-        const int2 d = A.cdesc[blockIdx.x];
+        const int2 d = A.cdesc[bid];
         if (d.y < 0) return;  // no rows left for this workgroup (uniform: before any barrier)
-        c_g0 = (unsigned)(blockIdx.x / A.wpc) * (unsigned)A.S + (unsigned)d.x;
+        c_g0 = (unsigned)(bid / A.wpc) * (unsigned)A.S + (unsigned)d.x;
         c_ng = d.y & 255;
         c_flags = d.y >> 8;
     }
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
     if (A.pool_mode == 1 || compact)
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
-    const unsigned g0 = compact ? c_g0 : (unsigned)(blockIdx.x * kChainRows) / (unsigned)A.K;  // first group
+    const unsigned g0 = compact ? c_g0 : (unsigned)(bid * kChainRows) / (unsigned)A.K;  // first group
     float *ulds = reinterpret_cast<float *>(csm + A.lds_u);
     if constexpr (KB0M < 0) {
         // u[g][c] = sum_k W0[c][xyz k] * centroid[g][k]: the centroid's share of layer 0, which
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     if (compact) {
         // unit i of the workgroup = rows 8(i%4).. of wave i/4; a row past the unit's distinct
         // neighbours takes the unit's first (a distinct neighbour of the same group)
-        urow_e = A.cunits[blockIdx.x * kUnitsPerWG + wave * 4 + (r >> 3)];
+        urow_e = A.cunits[bid * kUnitsPerWG + wave * 4 + (r >> 3)];
         valid = urow_e >= 0;
         const int k = (urow_e >> 4) & 15, nv = (urow_e & 7) + 1;
         g = valid ? c_g0 + (unsigned)(urow_e >> 8) : c_g0;
@@ -536,7 +539,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             if (h == 0 && (unsigned)slab * 32u < (unsigned)A.M) {
                 if (A.pool_mode == 0) A.out[(int64_t)gg * A.ostride + col] = m;
                 else if (A.pool_mode == 1)
-                    atomicMax(&cpool[(int)(gg - (unsigned)blockIdx.x * gpb) * coutL + col], __float_as_uint(m));
+                    atomicMax(&cpool[(int)(gg - (unsigned)bid * gpb) * coutL + col], __float_as_uint(m));
                 else
                     atomicMax(reinterpret_cast<unsigned *>(A.out + (int64_t)gg * A.ostride + col), __float_as_uint(m));
             }
@@ -559,7 +562,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         __syncthreads();
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) {
             const int gl = e / coutL, c = e - gl * coutL;
-            const unsigned gg = (unsigned)blockIdx.x * gpb + gl;
+            const unsigned gg = (unsigned)bid * gpb + gl;
             if (gg < G) A.out[(int64_t)gg * A.ostride + c] = __uint_as_float(cpool[e]);
         }
     }

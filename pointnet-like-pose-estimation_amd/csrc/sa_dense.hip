@@ -81,8 +81,12 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
     const int lane = tid & 63;
     const int r = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int row0 = blockIdx.x * kDRows;
-    const int ct0 = blockIdx.y * NTC;  // first output tile
+    // logical (row block, column tiles) with the row blocks in contiguous ranges per XCD: the
+    // next layer's row block runs on the XCD whose L2 holds its rows (and the SA chain's
+    // workgroups of a cloud on the one whose L2 holds the cloud's pre-pass rows)
+    const unsigned lid = xcd_contiguous(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+    const int row0 = (int)(lid / gridDim.y) * kDRows;
+    const int ct0 = (int)(lid % gridDim.y) * NTC;  // first output tile
     const int ncols = 32 * NTC;
     char *stages = dsm;
     float *opool = reinterpret_cast<float *>(dsm + 2 * kStage);  // [groups][ncols]

@@ -13,6 +13,8 @@ flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I" + os.path.j
          "--offload-device-only"]
 if os.path.basename(src) not in ("sa_mlp.hip", "sa_chain.hip", "sa_dense.hip", "linear.hip"):
     flags.append("-ffp-contract=off")
+if os.path.basename(src) == "sa_dense.hip":  # csrc/Makefile DENSEFLAGS
+    flags += ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 out = subprocess.run(["/opt/rocm/bin/hipcc"] + flags, capture_output=True, text=True).stderr
 cur = None
 rows = {}
