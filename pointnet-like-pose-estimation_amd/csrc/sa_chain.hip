@@ -78,6 +78,20 @@ struct ChainArgs {
     int wpc;  // workgroups per cloud
 };
 
+// Timeline stamps (diagnostic builds only: -DPN2_CHAIN_STAMPS, tools/debug/chain_stamps.py):
+// s_memrealtime (100 MHz, chip-wide) at fixed points of every workgroup, wave 0 lane 0.
+#ifdef PN2_CHAIN_STAMPS
+constexpr int kStampWG = 16384, kStamps = 6;
+__device__ unsigned long long g_chain_stamps[kStampWG * kStamps];
+#define PN2_STAMP(i)                                                                          \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < kStampWG)                                        \
+            g_chain_stamps[blockIdx.x * kStamps + (i)] = __builtin_amdgcn_s_memrealtime();    \
+    } while (0)
+#else
+#define PN2_STAMP(i) do {} while (0)
+#endif
+
 constexpr int kUnitRows = 8;
 constexpr int kUnitsPerWG = kChainRows / kUnitRows;  // 16
 
@@ -192,6 +206,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // a cloud's workgroups on one XCD: its rows gather the same points (and the pre-pass wrote
     // that cloud's z rows from the same XCD, see sa_dense.hip)
+    PN2_STAMP(0);
     const int bid = (int)xcd_contiguous(blockIdx.x, gridDim.x);
     const int slab = bid * kChainWaves + wave;
     const pn2_sa_src &s = A.src;
@@ -202,83 +217,16 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     int c_ng = 0, c_flags = 0;
     if (compact) {
         const int2 d = A.cdesc[bid];
-        if (d.y < 0) return;  // no rows left for this workgroup (uniform: before any barrier)
+        if (d.y < 0) {  // no rows left for this workgroup (uniform: before any barrier)
+            PN2_STAMP(5);
+            return;
+        }
         c_g0 = (unsigned)(bid / A.wpc) * (unsigned)A.S + (unsigned)d.x;
         c_ng = d.y & 255;
         c_flags = d.y >> 8;
     }
     // groups per workgroup of the LDS pool (pool_mode 1; compact: up to one per unit)
     const int gpb = compact ? kUnitsPerWG : kChainRows / A.K;
-
-    // stage BN scale/shift of the three layers: [al0|be0|al1|be1|al2|be2]
-    float *bn = reinterpret_cast<float *>(csm + A.lds_bn);
-    float *al0 = bn, *be0 = al0 + 32 * T0, *al1 = be0 + 32 * T0, *be1 = al1 + 32 * T1;
-    float *al2 = be1 + 32 * T1, *be2 = al2 + coutL;
-    for (int e = tid; e < 32 * T0; e += 64 * kChainWaves) { al0[e] = L0.alpha[e]; be0[e] = L0.beta[e]; }
-    for (int e = tid; e < 32 * T1; e += 64 * kChainWaves) { al1[e] = L1.alpha[e]; be1[e] = L1.beta[e]; }
-    for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
-    if (A.pool_mode == 1 || compact)
-        for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
-    const unsigned g0 = compact ? c_g0 : (unsigned)(bid * kChainRows) / (unsigned)A.K;  // first group
-    float *ulds = reinterpret_cast<float *>(csm + A.lds_u);
-    if constexpr (KB0M < 0) {
-        // u[g][c] = sum_k W0[c][xyz k] * centroid[g][k]: the centroid's share of layer 0, which
-        // the per-point pre-pass (z) could not subtract
-        const unsigned Gn = (unsigned)A.M / (unsigned)A.K;
-        for (int e = tid; e < A.u_groups * 32 * T0; e += 64 * kChainWaves) {
-            const int gl = e / (32 * T0), c = e - gl * (32 * T0);
-            const unsigned g = g0 + gl;
-            float u = 0.f;
-            if (g < Gn)
-                for (int k = 0; k < A.C; ++k) {
-                    const int row = A.w0x_row + k;
-                    u = __builtin_fmaf(A.w0x[((int64_t)(row >> 1) * (32 * T0) + c) * 2 + (row & 1)],
-                                       A.src.ctr[(int64_t)g * A.C + k], u);
-                }
-            ulds[e] = u;
-        }
-    }
-    __syncthreads();
-    char *ring = csm + A.lds_ring;
-    const unsigned loff = (unsigned)lane * 16u;
-    // Ring steps in consumption order: layers 0 (resident input only) and 1 block-major, layer 2
-    // tile-major; source addresses come from scalar arithmetic on the layer's base.
-    auto issue_l = [&](const ChainLayer &L, int t, int kb, char *dst) {
-        ring_issue<NP>(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64, dst, loff);
-    };
-    auto issue2 = [&](int z, char *dst) {  // layer-2 step z
-        z = min(z, L2.tiles * KB2 - 1);
-        issue_l(L2, z / KB2, z % KB2, dst);
-    };
-    auto issue1 = [&](int y, char *dst) {  // layer-1 step y (block-major)
-        if (y < T1 * KB1) issue_l(L1, y % T1, y / T1, dst);
-        else issue2(y - T1 * KB1, dst);
-    };
-    const int n0 = T0 * L0.kb;
-    auto issue_stage = [&](int st) {  // this wave's step of stage st
-        const int x = st * kChainWaves + wave;
-        char *dst = ring + (st % KS) * kStageBytes + wave * kStepBytes;
-        if constexpr (KB0M > 0) {
-            if (x < n0) issue_l(L0, x % T0, x / T0, dst);
-            else issue1(x - n0, dst);
-        } else {
-            issue1(x, dst);
-        }
-    };
-    int nread = 0;
-    auto read_w = [&]() {
-        if ((nread & (kChainWaves - 1)) == 0) {  // first step of a stage
-            const int st = nread / kChainWaves;
-            ring_fence();
-            stage_wait<NP, KS>();
-            stage_barrier();
-            issue_stage(st + KS - 1);
-        }
-        const Split w = ring_readN<NP>(ring + ((nread / kChainWaves) % KS) * kStageBytes +
-                                      (nread & (kChainWaves - 1)) * kStepBytes, lane);
-        ++nread;
-        return w;
-    };
 
     // ---- this lane's row: (group g, batch b, point n)
     unsigned g;
@@ -331,6 +279,102 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
     };
 
+    // The row gather (unit table -> neighbour index -> point / feature / pre-pass row: a chain
+    // of dependent loads) is issued here, before the BN staging and its barrier, so its latency
+    // overlaps the setup instead of following it (tools/debug/chain_stamps.py: the gather was
+    // ~28 % of a workgroup's life at SSG sa1).
+    float x0[KB0M > 0 ? KB0M : 1][8];  // KB0M > 0: the whole layer-0 input
+    float xs0[8];                       // KB0M == 0: its first block
+    cfloatx4 zc[4];                     // KB0M < 0: tile 0 of the row's pre-pass z
+    if constexpr (KB0M > 0) {
+#pragma unroll
+        for (int kb = 0; kb < KB0M; ++kb) {
+            if (kb < L0.kb) {
+                load_x(kb, x0[kb]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x0[kb][j] = 0.f;
+            }
+        }
+    } else if constexpr (KB0M == 0) {
+        load_x(0, xs0);
+    } else {
+        const float *zrow0 = A.z + ((int64_t)b * s.N + n) * (32 * T0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) zc[m] = *reinterpret_cast<const cfloatx4 *>(zrow0 + 4 * h + 8 * m);
+    }
+
+    // stage BN scale/shift of the three layers: [al0|be0|al1|be1|al2|be2]
+    float *bn = reinterpret_cast<float *>(csm + A.lds_bn);
+    float *al0 = bn, *be0 = al0 + 32 * T0, *al1 = be0 + 32 * T0, *be1 = al1 + 32 * T1;
+    float *al2 = be1 + 32 * T1, *be2 = al2 + coutL;
+    for (int e = tid; e < 32 * T0; e += 64 * kChainWaves) { al0[e] = L0.alpha[e]; be0[e] = L0.beta[e]; }
+    for (int e = tid; e < 32 * T1; e += 64 * kChainWaves) { al1[e] = L1.alpha[e]; be1[e] = L1.beta[e]; }
+    for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
+    if (A.pool_mode == 1 || compact)
+        for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
+    const unsigned g0 = compact ? c_g0 : (unsigned)(bid * kChainRows) / (unsigned)A.K;  // first group
+    float *ulds = reinterpret_cast<float *>(csm + A.lds_u);
+    if constexpr (KB0M < 0) {
+        // u[g][c] = sum_k W0[c][xyz k] * centroid[g][k]: the centroid's share of layer 0, which
+        // the per-point pre-pass (z) could not subtract
+        const unsigned Gn = (unsigned)A.M / (unsigned)A.K;
+        for (int e = tid; e < A.u_groups * 32 * T0; e += 64 * kChainWaves) {
+            const int gl = e / (32 * T0), c = e - gl * (32 * T0);
+            const unsigned g = g0 + gl;
+            float u = 0.f;
+            if (g < Gn)
+                for (int k = 0; k < A.C; ++k) {
+                    const int row = A.w0x_row + k;
+                    u = __builtin_fmaf(A.w0x[((int64_t)(row >> 1) * (32 * T0) + c) * 2 + (row & 1)],
+                                       A.src.ctr[(int64_t)g * A.C + k], u);
+                }
+            ulds[e] = u;
+        }
+    }
+    __syncthreads();
+    PN2_STAMP(1);
+    char *ring = csm + A.lds_ring;
+    const unsigned loff = (unsigned)lane * 16u;
+    // Ring steps in consumption order: layers 0 (resident input only) and 1 block-major, layer 2
+    // tile-major; source addresses come from scalar arithmetic on the layer's base.
+    auto issue_l = [&](const ChainLayer &L, int t, int kb, char *dst) {
+        ring_issue<NP>(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64, dst, loff);
+    };
+    auto issue2 = [&](int z, char *dst) {  // layer-2 step z
+        z = min(z, L2.tiles * KB2 - 1);
+        issue_l(L2, z / KB2, z % KB2, dst);
+    };
+    auto issue1 = [&](int y, char *dst) {  // layer-1 step y (block-major)
+        if (y < T1 * KB1) issue_l(L1, y % T1, y / T1, dst);
+        else issue2(y - T1 * KB1, dst);
+    };
+    const int n0 = T0 * L0.kb;
+    auto issue_stage = [&](int st) {  // this wave's step of stage st
+        const int x = st * kChainWaves + wave;
+        char *dst = ring + (st % KS) * kStageBytes + wave * kStepBytes;
+        if constexpr (KB0M > 0) {
+            if (x < n0) issue_l(L0, x % T0, x / T0, dst);
+            else issue1(x - n0, dst);
+        } else {
+            issue1(x, dst);
+        }
+    };
+    int nread = 0;
+    auto read_w = [&]() {
+        if ((nread & (kChainWaves - 1)) == 0) {  // first step of a stage
+            const int st = nread / kChainWaves;
+            ring_fence();
+            stage_wait<NP, KS>();
+            stage_barrier();
+            issue_stage(st + KS - 1);
+        }
+        const Split w = ring_readN<NP>(ring + ((nread / kChainWaves) % KS) * kStageBytes +
+                                      (nread & (kChainWaves - 1)) * kStepBytes, lane);
+        ++nread;
+        return w;
+    };
+
     Split X1[2 * T0];
     if constexpr (KB0M < 0) {
         // ---- layer 0 pre-transformed: acc = z[point] - u[group], already in the transposed
@@ -343,7 +387,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         // loads are read-only, so the compiler would hoist every tile's loads to the top and
         // spill at 2 waves/SIMD: the address of tile t+1 is tied (opaque asm) to tile t-1's
         // result, which bounds the loads in flight to two tiles.
-        cfloatx4 zc[4], uc[4];
+        cfloatx4 uc[4];
         auto load_tile = [&](int o, cfloatx4 (&zq)[4], cfloatx4 (&uq)[4]) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -351,7 +395,8 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
                 uq[m] = *reinterpret_cast<const cfloatx4 *>(urow + o + 8 * m);
             }
         };
-        load_tile(4 * h, zc, uc);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) uc[m] = *reinterpret_cast<const cfloatx4 *>(urow + 4 * h + 8 * m);
         unsigned dep = 0;
 #pragma unroll
         for (int t = 0; t < T0; ++t) {
@@ -380,16 +425,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     } else if constexpr (KB0M > 0) {
         // ---- layer 0 from registers: the whole input gathered once (raw fp32), then k-outer
         // (each block split once, every output tile accumulating) with weights from the ring
-        float x[KB0M][8];
-#pragma unroll
-        for (int kb = 0; kb < KB0M; ++kb) {
-            if (kb < L0.kb) {
-                load_x(kb, x[kb]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) x[kb][j] = 0.f;
-            }
-        }
+        auto &x = x0;  // gathered before the setup
 #pragma unroll
         for (int st = 0; st < KS - 1; ++st) issue_stage(st);  // overlaps the gather's latency
         cfloatx16 acc[T0];
@@ -418,7 +454,8 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
         float xn[8];
-        load_x(0, xn);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xn[j] = xs0[j];  // block 0, gathered before the setup
         for (int kb = 0; kb < L0.kb; ++kb) {
             float x[8];
 #pragma unroll
@@ -438,6 +475,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
     }
 
+    PN2_STAMP(2);
     // ---- layer 1: input in registers, k-outer (each input block dies after its use, so X1 and
     // X2 are never both whole in registers), every output tile accumulating (transposed)
     Split X2[2 * T1];
@@ -455,6 +493,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         for (int t = 0; t < T1; ++t) hidden_epilogue<NP>(acc[t], al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
     }
 
+    PN2_STAMP(3);
     // ---- layer 2: standard orientation, pooled over the neighbourhood
     const unsigned G = (unsigned)A.M / (unsigned)A.K;
     for (int t = 0; t < L2.tiles; ++t) {
@@ -546,6 +585,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing (repeat) copies
+    PN2_STAMP(4);
     if (compact) {
         __syncthreads();
         // a group shared with the neighbouring workgroup is merged by atomicMax into its row
@@ -566,6 +606,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             if (gg < G) A.out[(int64_t)gg * A.ostride + c] = __uint_as_float(cpool[e]);
         }
     }
+    PN2_STAMP(5);
 }
 
 // hidden-width signatures (output tiles of layers 0 and 1) compiled; the reference heads use
@@ -739,6 +780,14 @@ __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
 }
 
 // ------------------------------------------------------------------ host: dispatch
+
+#ifdef PN2_CHAIN_STAMPS
+// copy the stamps of the last chain launch out (diagnostic builds only)
+extern "C" int pn2_debug_chain_stamps(unsigned long long *dst, int64_t n) {
+    const int64_t m = n < (int64_t)kStampWG * kStamps ? n : (int64_t)kStampWG * kStamps;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_chain_stamps), m * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 static int compact_stages() {
     const char *e = getenv("PN2_COMPACT_KS");
