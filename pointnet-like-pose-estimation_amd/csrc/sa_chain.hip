@@ -60,12 +60,10 @@ struct ChainArgs {
     int lds_bn;    // byte offset of the staged BN scale/shift
     int lds_ring;  // byte offset of the workgroup weight ring (kStages stage buffers)
     // KB0M < 0 (layer 0 pre-transformed): z [B*N][32*T0] = W0 . [xyz | features] of every source
-    // point (launch_layer0_prepass); the xyz columns of W0 in the fp32 image `wt` (input channel
-    // k of xyz at row w0x_row + k); u [groups][32*T0] = W0_xyz . centroid staged at lds_u
+    // point (launch_layer0_prepass); u [B*S][32*T0] = W0_xyz . centroid of every group
+    // (u_table_kernel)
     const float *z;
-    const float *w0x;
-    int w0x_row;
-    int lds_u, u_groups;
+    const float *u;
     // compact neighbourhoods (pool_mode 3, given the ball query's distinct-neighbour counts): a
     // group's rows past its distinct neighbours repeat its first neighbour
     // (pointnet2_utils.py:87-89), and the max over the group is the same without them -- so
@@ -285,7 +283,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     // ~28 % of a workgroup's life at SSG sa1).
     float x0[KB0M > 0 ? KB0M : 1][8];  // KB0M > 0: the whole layer-0 input
     float xs0[8];                       // KB0M == 0: its first block
-    cfloatx4 zc[4];                     // KB0M < 0: tile 0 of the row's pre-pass z
+    cfloatx4 zc[4], uc[4];              // KB0M < 0: tile 0 of the row's z and its group's u
     if constexpr (KB0M > 0) {
 #pragma unroll
         for (int kb = 0; kb < KB0M; ++kb) {
@@ -300,8 +298,12 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         load_x(0, xs0);
     } else {
         const float *zrow0 = A.z + ((int64_t)b * s.N + n) * (32 * T0);
+        const float *urow0 = A.u + (int64_t)g * (32 * T0);
 #pragma unroll
-        for (int m = 0; m < 4; ++m) zc[m] = *reinterpret_cast<const cfloatx4 *>(zrow0 + 4 * h + 8 * m);
+        for (int m = 0; m < 4; ++m) {
+            zc[m] = *reinterpret_cast<const cfloatx4 *>(zrow0 + 4 * h + 8 * m);
+            uc[m] = *reinterpret_cast<const cfloatx4 *>(urow0 + 4 * h + 8 * m);
+        }
     }
 
     // stage BN scale/shift of the three layers: [al0|be0|al1|be1|al2|be2]
@@ -313,25 +315,6 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
     if (A.pool_mode == 1 || compact)
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
-    const unsigned g0 = compact ? c_g0 : (unsigned)(bid * kChainRows) / (unsigned)A.K;  // first group
-    float *ulds = reinterpret_cast<float *>(csm + A.lds_u);
-    if constexpr (KB0M < 0) {
-        // u[g][c] = sum_k W0[c][xyz k] * centroid[g][k]: the centroid's share of layer 0, which
-        // the per-point pre-pass (z) could not subtract
-        const unsigned Gn = (unsigned)A.M / (unsigned)A.K;
-        for (int e = tid; e < A.u_groups * 32 * T0; e += 64 * kChainWaves) {
-            const int gl = e / (32 * T0), c = e - gl * (32 * T0);
-            const unsigned g = g0 + gl;
-            float u = 0.f;
-            if (g < Gn)
-                for (int k = 0; k < A.C; ++k) {
-                    const int row = A.w0x_row + k;
-                    u = __builtin_fmaf(A.w0x[((int64_t)(row >> 1) * (32 * T0) + c) * 2 + (row & 1)],
-                                       A.src.ctr[(int64_t)g * A.C + k], u);
-                }
-            ulds[e] = u;
-        }
-    }
     __syncthreads();
     PN2_STAMP(1);
     char *ring = csm + A.lds_ring;
@@ -382,12 +365,11 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int st = 0; st < KS - 1; ++st) issue_stage(st);
         const float *zrow = A.z + ((int64_t)b * s.N + n) * (32 * T0);
-        const float *urow = ulds + (int)(g - g0) * (32 * T0);
+        const float *urow = A.u + (int64_t)g * (32 * T0);
         // Tile t+1's z / u loads are issued while tile t is split (one tile of lookahead).  The
         // loads are read-only, so the compiler would hoist every tile's loads to the top and
         // spill at 2 waves/SIMD: the address of tile t+1 is tied (opaque asm) to tile t-1's
         // result, which bounds the loads in flight to two tiles.
-        cfloatx4 uc[4];
         auto load_tile = [&](int o, cfloatx4 (&zq)[4], cfloatx4 (&uq)[4]) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
@@ -395,8 +377,6 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
                 uq[m] = *reinterpret_cast<const cfloatx4 *>(urow + o + 8 * m);
             }
         };
-#pragma unroll
-        for (int m = 0; m < 4; ++m) uc[m] = *reinterpret_cast<const cfloatx4 *>(urow + 4 * h + 8 * m);
         unsigned dep = 0;
 #pragma unroll
         for (int t = 0; t < T0; ++t) {
@@ -779,6 +759,24 @@ __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
     }
 }
 
+// u [g][c] = sum_k W0[c][xyz k] * centroid[g][k] (k ascending, one fma chain from 0): the
+// centroid's share of layer 0, which the per-point pre-pass z could not subtract.  W0's fp32
+// image is pair-interleaved [cin_pad/2][cout][2]; its xyz rows start at w0x_row.
+__global__ __launch_bounds__(256) void u_table_kernel(const float *__restrict__ w0x, int w0x_row,
+                                                      int cout, const float *__restrict__ ctr,
+                                                      int C, int64_t G, float *__restrict__ u) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= G * cout) return;
+    const int64_t g = e / cout;
+    const int c = (int)(e - g * cout);
+    float acc = 0.f;
+    for (int k = 0; k < C; ++k) {
+        const int row = w0x_row + k;
+        acc = __builtin_fmaf(w0x[((int64_t)(row >> 1) * cout + c) * 2 + (row & 1)], ctr[g * C + k], acc);
+    }
+    u[e] = acc;
+}
+
 // ------------------------------------------------------------------ host: dispatch
 
 #ifdef PN2_CHAIN_STAMPS
@@ -854,7 +852,7 @@ static bool chain_shape(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nl
 
 // compact neighbourhoods (pool_mode 3): groups of K in [9, 128] (K <= 8 is one unit anyway),
 // given the ball query's counts, the scan kernel's LDS within one CU's 160 KB.  PN2_COMPACT=0
-// disables (A/B), =1 also compacts pre-pass chains; PN2_COMPACT_KS=3 keeps the 3-stage ring.
+// disables (A/B); PN2_COMPACT_KS=3 keeps the 3-stage ring.
 static int64_t compact_wpc(const pn2_sa_src &s) {
     return (s.S * ((s.K + kUnitRows - 1) / kUnitRows) + kUnitsPerWG - 1) / kUnitsPerWG;
 }
@@ -872,7 +870,15 @@ static int64_t compact_table_bytes(const pn2_sa_src &s) {
     return s.B * compact_wpc(s) * (kUnitsPerWG * 4 + 8);
 }
 
-// workspace of a chain launch: [layer-0 pre-pass z | compact unit table | compact descriptors]
+// the pre-pass tables: z [B*N][cout0] and u [B*S][cout0], 16-byte aligned each
+static int64_t prepass_z_bytes(const pn2_sa_src &s, const pn2_mlp_layer &L0) {
+    return (s.B * s.N * L0.cout * 4 + 15) / 16 * 16;
+}
+static int64_t prepass_bytes(const pn2_sa_src &s, const pn2_mlp_layer &L0) {
+    return prepass_z_bytes(s, L0) + (s.B * s.S * L0.cout * 4 + 15) / 16 * 16;
+}
+
+// workspace of a chain launch: [pre-pass z | pre-pass u | compact unit table | descriptors]
 int64_t chain_prepass_bytes(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np) {
     int T0, T1, kbs[3];
     if (!chain_shape(s, layers, nlayers, 1, T0, T1, kbs)) return 0;
@@ -880,7 +886,7 @@ int64_t chain_prepass_bytes(const pn2_sa_src &s, const pn2_mlp_layer *layers, in
     const int64_t M = s.B * s.S * s.K;
     int64_t bytes = 0;
     if (chain_use_prepass(s, layers, T0, T1, kbs[0], M, np))
-        bytes += (s.B * s.N * layers[0].cout * 4 + 15) / 16 * 16;
+        bytes += prepass_bytes(s, layers[0]);
     if (chain_use_compact(s)) bytes += compact_table_bytes(s);
     return bytes;
 }
@@ -899,23 +905,26 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     // without compaction a 32-row slab must hold rows of one group (K = 8, 16: several whole
     // groups; K % 32 == 0: part of one)
     if (!(pool && chain_use_compact(s)) && !(K == 8 || K == 16 || K % 32 == 0)) return 0;
-    const int64_t zbytes = (s.B * s.N * layers[0].cout * 4 + 15) / 16 * 16;
+    const int64_t pbytes = prepass_bytes(s, layers[0]);
     const bool pre = chain_use_prepass(s, layers, T0, T1, kbs[0], M, np) && ws &&
-                     ws_bytes >= zbytes && ((uintptr_t)ws & 15) == 0;
-    const int64_t zb = pre ? zbytes : 0;
+                     ws_bytes >= pbytes && ((uintptr_t)ws & 15) == 0;
+    const int64_t zb = pre ? pbytes : 0;
     bool compact = pool && chain_use_compact(s) && ws && ((uintptr_t)ws & 15) == 0 &&
                    ws_bytes >= zb + compact_table_bytes(s);
-    // With the layer-0 pre-pass (wide first layers: SSG / pose sa2) the group pool and the u
-    // table of a compact launch cost a weight-ring stage or an occupancy step, which measured
-    // slower than computing the padding rows (SSG sa2: 143 / 160 us vs 131 us): compact only
-    // without it unless PN2_COMPACT=1.
-    if (pre) {
-        const char *e = getenv("PN2_COMPACT");
-        if (!(e && strcmp(e, "1") == 0)) compact = false;
-    }
+    // With the layer-0 pre-pass (wide first layers: SSG / pose sa2) compaction paid only once
+    // the centroid term u came from a global table (u_table_kernel) instead of being computed
+    // per workgroup for its 16 groups (setup 8.8 us of a 49 us workgroup life,
+    // tools/debug/chain_stamps.py): SSG sa2 115 us vs 130 us computing the padding rows.
+    float *utab = pre ? reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + prepass_z_bytes(s, layers[0]))
+                      : nullptr;
     if (pre) {
         const int rc = launch_layer0_prepass(s, layers[0], ws, st);
         if (rc != PN2_OK) return rc;
+        const int64_t G = s.B * s.S, cout0 = layers[0].cout;
+        hipLaunchKernelGGL(u_table_kernel, dim3((unsigned)((G * cout0 + 255) / 256)), dim3(256), 0, st,
+                           layers[0].wt, (int)(layers[0].cin - s.C), (int)cout0, s.ctr, (int)s.C, G,
+                           utab);  // the fp32 image's rows are [features | xyz]
+        PN2_LAUNCH_CHECK("u_table_kernel");
         KB0M = -1;
     }
     const int wpc = compact ? (int)compact_wpc(s) : 0;
@@ -958,8 +967,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     A.wpc = wpc;
     if (pre) {
         A.z = ws;
-        A.w0x = layers[0].wt;
-        A.w0x_row = (int)(layers[0].cin - s.C);  // the fp32 image's rows are [features | xyz]
+        A.u = utab;
     }
     const int64_t coutL = layers[2].cout;
     size_t lds = 0;
@@ -988,11 +996,6 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     const size_t bn_bytes = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + coutL);
     A.lds_ring = (int)((A.lds_bn + bn_bytes + 15) / 16 * 16);
     lds = (size_t)A.lds_ring + (size_t)(compact ? compact_stages() : kStages) * (np == 3 ? stage_bytes<3>() : stage_bytes<1>());
-    if (pre) {  // u for every group a workgroup's rows touch
-        A.u_groups = compact ? kUnitsPerWG : (int)((kChainRows + K - 1) / K + 1);
-        A.lds_u = (int)((lds + 15) / 16 * 16);
-        lds = (size_t)A.lds_u + (size_t)A.u_groups * layers[0].cout * 4;
-    }
     int rc = PN2_EUNSUPPORTED;
 #define PN2_CHAIN_GO(a, b, c)                                                             \
     if (T0 == a && T1 == b && KB0M == c)                                                  \

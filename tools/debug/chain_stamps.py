@@ -78,6 +78,13 @@ def main():
         model.sa2(l1p, l1f)
         st2 = stamps()
         report("sa2 (pre-pass, KB0M=-1)", st2, 32 * 128 * 64 // 128)
+        # the compact variant of sa2 (PN2_COMPACT=1: distinct rows only, 8-row units)
+        os.environ["PN2_COMPACT"] = "1"
+        model.sa2(l1p, l1f)
+        model.sa2(l1p, l1f)
+        st3 = stamps()
+        report("sa2 compact (PN2_COMPACT=1)", st3, 32 * 128 * 64 // 128)
+        del os.environ["PN2_COMPACT"]
 
 
 if __name__ == "__main__":
