@@ -23,7 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CALLS_PER_FORWARD = {"ssg": 3, "msg": 7, "pose": 6, "stress": 3}
 FORWARD_MARKER = "fps_kernel"  # one launch per sampled SA layer, counted below
 # kernels one pn2_sa_mlp_max_f32 call may dispatch
-MLP_KERNELS = ("sa_mlp_kernel", "dense_layer_kernel", "sa_chain_kernel", "dense_split_kernel")
+MLP_KERNELS = ("sa_mlp_kernel", "dense_layer_kernel", "sa_chain_kernel", "dense_split_kernel",
+               "compact_scan_kernel", "u_table_kernel")
 FPS_PER_FORWARD = {"ssg": 2, "msg": 2, "pose": 4, "stress": 2}
 
 
