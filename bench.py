@@ -85,13 +85,16 @@ def parse():
                     help="eager pipeline: run the head on its own stream (default off there)")
     ap.add_argument("--no-tail", action="store_true",
                     help="graphed pipeline: keep the head on the compute stream")
-    ap.add_argument("--slots", type=int, default=6,
+    ap.add_argument("--slots", type=int, default=8,
                     help="graphed pipeline: batch slots (a multiple of --geometry-batches; the "
                          "geometry runs slots/geometry-batches - 1 groups ahead)")
+    ap.add_argument("--compute-streams", type=int, default=None,
+                    help="graphed pipeline: consecutive batches' forwards alternate between this "
+                         "many compute streams (1 or 2; default 2 with shared CUs)")
     ap.add_argument("--geometry-batches", type=int, default=2,
                     help="graphed pipeline: consecutive batches whose geometry (FPS + ball "
                          "queries) runs as one replay over their clouds side by side")
-    ap.add_argument("--geometry-streams", type=int, default=2,
+    ap.add_argument("--geometry-streams", type=int, default=1,
                     help="graphed pipeline: 2 = consecutive batches' FPS chains on two streams")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="plain eager steps (default for single-head configs: pn2.pipeline)")
@@ -327,7 +330,8 @@ def main():
             pf = GraphedPipeline(pmodel, geometry_cus=a.geometry_cus,
                                  tail=not a.no_tail, nslots=a.slots,
                                  geometry_streams=a.geometry_streams,
-                                 geometry_batches=a.geometry_batches)
+                                 geometry_batches=a.geometry_batches,
+                                 compute_streams=a.compute_streams)
         else:
             pf = PipelinedForward(pmodel, geometry_cus=a.geometry_cus,
                                   tail="auto" if a.tail else False)
@@ -440,7 +444,8 @@ def main():
                                a.tail and not names[0].startswith("translation")) else "",
                            " on %d dedicated CUs" % a.geometry_cus if a.geometry_cus > 0
                            else "s sharing all CUs") + (
-                           "; geometry of %d batches per replay" % a.geometry_batches
+                           "; geometry of %d batches per replay" % a.geometry_batches +
+                           ("; %d compute streams" % pf.compute_streams)
                            if not a.eager_pipeline else "")
                        if pipelined else "eager"),
             "eager_value": round(eager_value, 2),

@@ -72,7 +72,12 @@ __global__ void unkey_kernel(float *out, int64_t ostride, int64_t G, int cols) {
     *p = funkey(__float_as_uint(*p));
 }
 
-template <int NTC, int NP>
+// one lane-linear 16-byte-per-lane copy HBM/L2 -> LDS (global_load_lds, no VGPR destination)
+__device__ __forceinline__ void dma16(const char *src, char *dst) {
+    __builtin_amdgcn_global_load_lds(src, (lds_void *)dst, 16, 0, 0);
+}
+
+template <int NTC, int NP, bool FAST>
 __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitArgs A) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     constexpr int kFrag = NP * NTC;                  // fragments per k-block
@@ -138,20 +143,62 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
         }
     };
 
+    // FAST: every k-block past the first stage is 16 contiguous channels of one row run, at
+    // lrow + 16 kb (rows mode: the row; group_all: the features, blocks >= 1) -- two 16-byte
+    // loads at immediate offsets from one pointer per stage, no per-element branches
+    const float *lrow = A.mode == 0 ? arow : frow - 16;
+    lrow += 4 * h;
+    auto load_fast = [&](int c, float (&x)[kKC][8]) {
+        const int kb0 = c * kKC;
+        if (kb0 + kKC <= A.kb) {
+            const float *p = lrow + 16 * kb0;
+#pragma unroll
+            for (int k = 0; k < kKC; ++k)
+#pragma unroll
+                for (int run = 0; run < 2; ++run) {
+                    const cfloatx4 q = *reinterpret_cast<const cfloatx4 *>(p + 16 * k + 8 * run);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[k][4 * run + i] = q[i];
+                }
+        } else {  // the last, partial stage: blocks past the input are never multiplied
+#pragma unroll
+            for (int k = 0; k < kKC; ++k) {
+                const float *p = lrow + 16 * min(kb0 + k, A.kb - 1);
+#pragma unroll
+                for (int run = 0; run < 2; ++run) {
+                    const cfloatx4 q = *reinterpret_cast<const cfloatx4 *>(p + 8 * run);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[k][4 * run + i] = q[i];
+                }
+            }
+        }
+    };
+
     // ---- weight stages: stage c = k-blocks [c*kKC, c*kKC + kKC) of this workgroup's NTC tiles,
-    // fragment (kbl, i, p) at ((kbl * NTC + i) * NP + p) KB
+    // fragment (kbl, i, p) at ((kbl * NTC + i) * NP + p) KB.  Wave w copies fragments w, w + kDW,
+    // ...; their source bases are wave-uniform and computed once, so a stage's copies cost a few
+    // scalar adds (the lane's 16-byte offset is the copy's only vector operand).
+    constexpr int kPer = kKC * kFrag / kDW;
+    static_assert(kKC * kFrag % kDW == 0, "fragments per wave");
     const int nst = (A.kb + kKC - 1) / kKC;
     const int64_t plane = (int64_t)A.tiles * A.kb * 64;
     const unsigned loff = (unsigned)lane * 16u;
+    const char *fsrc[kPer];
+    int fkbl[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int f = wave + kDW * j;
+        const int kbl = f / kFrag, rem = f - kbl * kFrag;
+        const int i = rem / NP, p = rem - NP * i;
+        fsrc[j] = reinterpret_cast<const char *>(A.w + p * plane + (int64_t)(ct0 + i) * A.kb * 64);
+        fkbl[j] = kbl;
+    }
     auto issue_stage = [&](int c) {
         char *buf = stages + (c & 1) * kStage;
-        for (int f = wave; f < kKC * kFrag; f += kDW) {
-            const int kbl = f / kFrag, rem = f - kbl * kFrag;
-            const int i = rem / NP, p = rem - NP * i;
-            const int kb = min(c * kKC + kbl, A.kb - 1);
-            const bf16x8 *src = A.w + p * plane + ((int64_t)(ct0 + i) * A.kb + kb) * 64;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const char *>(src) + loff,
-                                             (lds_void *)(buf + f * 1024), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int kb = min(c * kKC + fkbl[j], A.kb - 1);
+            dma16(fsrc[j] + (int64_t)kb * 1024 + loff, buf + (wave + kDW * j) * 1024);
         }
     };
 
@@ -160,30 +207,41 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
     for (int i = 0; i < NTC; ++i)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[i][q] = 0.f;
-    float xa[kKC][8];
+    // one stage: wait for stage c, prefetch stage c + 1 (rows into xn, weights by DMA), then
+    // the MFMAs of stage c from xc.  Stages alternate between two register sets (no copies).
+    auto step = [&](int c, float (&xc)[kKC][8], float (&xn)[kKC][8]) {
+        // this wave's rows and weight copies of stage c have landed (issued one stage ago; a
+        // real s_waitcnt the compiler's own wait insertion sees), then the barrier: stage c is
+        // whole in LDS and buffer (c+1)&1 is free again
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        __syncthreads();
+        if (c + 1 < nst) {
+            if constexpr (FAST) {
+                load_fast(c + 1, xn);
+            } else {
 #pragma unroll
-    for (int k = 0; k < kKC; ++k) load_a(k, xa[k]);
-    issue_stage(0);
-    for (int c = 0; c < nst; ++c) {
-        __syncthreads();  // stage c landed for every wave; buffer (c+1)&1 is free again
-        float xn[kKC][8];
-#pragma unroll
-        for (int k = 0; k < kKC; ++k) load_a((c + 1) * kKC + k, xn[k]);
-        if (c + 1 < nst) issue_stage(c + 1);
+                for (int k = 0; k < kKC; ++k) load_a((c + 1) * kKC + k, xn[k]);
+            }
+            issue_stage(c + 1);
+        }
         const char *buf = stages + (c & 1) * kStage;
 #pragma unroll
         for (int k = 0; k < kKC; ++k) {
             if (c * kKC + k < A.kb) {
-                const Split xs = splitN<NP>(xa[k]);
+                const Split xs = splitN<NP>(xc[k]);
 #pragma unroll
                 for (int i = 0; i < NTC; ++i)
                     acc[i] = mma_wb<NP>(xs, ring_readN<NP>(buf + (k * kFrag + NP * i) * 1024, lane), acc[i]);
             }
         }
+    };
+    float xa[kKC][8], xb[kKC][8];
 #pragma unroll
-        for (int k = 0; k < kKC; ++k)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) xa[k][j] = xn[k][j];
+    for (int k = 0; k < kKC; ++k) load_a(k, xa[k]);
+    issue_stage(0);
+    for (int c = 0; c < nst; c += 2) {
+        step(c, xa, xb);
+        if (c + 1 < nst) step(c + 1, xb, xa);
     }
 
     // ---- epilogue: lane = output column, register q = row (q&3) + 8(q>>2) + 4h of the slab
@@ -278,10 +336,14 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
 
 template <int NTC, int NP>
 static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
+    // every k-block after the first stage is one contiguous 16-channel run of the row
+    const bool fast = A.vec && (A.mode == 0 ? A.cin % 16 == 0 && A.kb * 16 == A.cin
+                                            : A.feat && A.D > 0 && A.D % 16 == 0 && A.kb == 1 + A.D / 16);
     const size_t lds = (size_t)2 * kKC * NP * NTC * 1024 +
                        (A.pool_mode == 1 ? (size_t)(kDRows / A.K) * 32 * NTC * 4 : 0);
     dim3 grid((unsigned)((A.M + kDRows - 1) / kDRows), (unsigned)(A.tiles / NTC));
-    hipLaunchKernelGGL((dense_split_kernel<NTC, NP>), grid, dim3(64 * kDW), lds, st, A);
+    if (fast) hipLaunchKernelGGL((dense_split_kernel<NTC, NP, true>), grid, dim3(64 * kDW), lds, st, A);
+    else hipLaunchKernelGGL((dense_split_kernel<NTC, NP, false>), grid, dim3(64 * kDW), lds, st, A);
     PN2_LAUNCH_CHECK("dense_split_kernel");
     return PN2_OK;
 }

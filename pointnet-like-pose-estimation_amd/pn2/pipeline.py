@@ -131,6 +131,16 @@ def _extra_geometry_streams(device, n):
     return have[:n]
 
 
+_compute_extra = {}
+
+
+def _extra_compute_stream(device):
+    """A second default-priority compute stream for GraphedPipeline(compute_streams=2)."""
+    if device not in _compute_extra:
+        _compute_extra[device] = torch.cuda.Stream(torch.device("cuda", device))
+    return _compute_extra[device]
+
+
 def partition(device, geometry_cus):
     """(geometry stream, compute stream) on `device`: `geometry_cus` CUs (rounded down to a
     multiple of the XCD count, at least one per XCD) for the FPS chain, all the others for
@@ -379,13 +389,22 @@ class GraphedPipeline(PipelinedForward):
     with fewer batches repeats its first batch's input in the empty places (no draws, results
     unused).  Outputs are cloned out of the static buffers on the stream that produced them.
 
-    geometry_streams=2 (default, shared CUs): consecutive groups' geometry replays alternate
-    between two high-priority streams.  More streams exceed the 4 hardware queues a process
-    gets (GPU_MAX_HW_QUEUES) with the compute and tail streams.
+    compute_streams=2 (default with shared CUs): consecutive batches' sa graphs alternate
+    between two compute streams, so one batch's short dependent kernels (scans, the pre-pass)
+    and its kernels' last partial waves of workgroups run beside the other batch's chains.
+    geometry_streams=2: consecutive groups' geometry replays alternate between two
+    high-priority streams.  A process gets 4 hardware queues (GPU_MAX_HW_QUEUES): one geometry
+    stream + two compute streams + the tail stream is the default; with two geometry streams
+    and two compute streams the head graphs run on their batch's compute stream after its sa
+    graph (no tail stream).  Measured (SSG B=32, 100 batches, clouds/s): 1 compute + 2 geometry
+    streams, 6 slots 95-96.7k; 2 compute + 1 geometry + tail, 8 slots 106-107k (MSG +12.6 %,
+    POSE +7.9 %, STRESS +2.8 %); 2 + 2, head on the compute streams, 8 slots 103-104k.  The slot
+    count matters beyond "enough": 2 + 1 at 4 / 6 / 8 / 12 / 16 slots gave 92 / 100 / 107 /
+    91 / 106k (unexplained; reproducible per count).
     """
 
-    def __init__(self, model, geometry_cus=0, tail=True, nslots=6, geometry_streams=2,
-                 geometry_batches=2):
+    def __init__(self, model, geometry_cus=0, tail=True, nslots=8, geometry_streams=1,
+                 geometry_batches=2, compute_streams=None):
         super().__init__(model, geometry_cus, bool(tail))
         gb = int(geometry_batches)
         if gb < 1:
@@ -400,6 +419,15 @@ class GraphedPipeline(PipelinedForward):
         # (measured: 3 geometry streams 42.8k clouds/s at SSG vs 76.1k with 2)
         if geometry_streams not in (1, 2):
             raise ValueError("pn2.pipeline: geometry_streams is 1 or 2")
+        if compute_streams is None:
+            compute_streams = 2 if geometry_cus <= 0 else 1
+        if compute_streams not in (1, 2):
+            raise ValueError("pn2.pipeline: compute_streams is 1 or 2")
+        if compute_streams == 2 and geometry_cus > 0:
+            raise ValueError("pn2.pipeline: compute_streams=2 needs shared CUs (geometry_cus=0)")
+        self.compute_streams = int(compute_streams)
+        # the head graphs get the tail stream while the queues allow it
+        self.head_on_tail = geometry_streams + self.compute_streams + 1 <= 4
         self.nslots = int(nslots)
         self.gb = gb
         self.ngroups = self.nslots // gb
@@ -561,10 +589,14 @@ class GraphedPipeline(PipelinedForward):
         ngr = (nbat + gb - 1) // gb  # groups this call
         geo, main, tail = _streams(dev.index, self.geometry_cus)
         geos = [geo] + _extra_geometry_streams(dev.index, self.geometry_streams - 1)
+        mains = [main] + ([_extra_compute_stream(dev.index)] if self.compute_streams == 2 else [])
         caller = torch.cuda.current_stream(dev)
-        for st in geos + [main, tail]:
+        for st in geos + mains + [tail]:
             st.wait_stream(caller)
-        ev_fps, ev_read = [None] * ng, [None] * ng  # per group slot
+        # per group slot: the fps replay's event, and the events after which the group's
+        # batches no longer read its inputs / geometry (one per batch: with two compute
+        # streams they finish on different streams)
+        ev_fps, ev_read = [None] * ng, [[] for _ in range(ng)]
         ev_head = [None] * (ng * gb)  # per batch slot
         starts = self._draw_all(ngr)
 
@@ -588,8 +620,9 @@ class GraphedPipeline(PipelinedForward):
                 # the group slot's previous batches are done with its inputs and geometry
                 # outputs: their sa graphs read them, and so did their head graphs when the
                 # split put a group_all layer there (sa3 reads sa2's centroids)
-                if ev_read[s] is not None:
-                    geo.wait_event(ev_read[s])
+                for e in ev_read[s]:
+                    geo.wait_event(e)
+                ev_read[s] = []
                 mark(js[0] - first, "geo0", geo)
                 for h, j in enumerate(js):
                     grp.halves[h].x.copy_(batches[j if j < len(batches) else js[0]],
@@ -610,6 +643,7 @@ class GraphedPipeline(PipelinedForward):
                 sl = self._slots[s].halves[h]
                 if h == 0 and g + ng - 1 < ngr:
                     issue_fps(g + ng - 1)
+                main = mains[(i - first) % len(mains)]
                 with torch.cuda.stream(main):
                     main.wait_event(ev_fps[s])
                     if ev_head[bs] is not None:  # the batch slot's last head is done with the pool
@@ -620,17 +654,18 @@ class GraphedPipeline(PipelinedForward):
                     sl.sa.replay()
                     ev_sa = main.record_event()
                     mark(i - first, "sa1", main)
-                ts = tail if sl.head is not None else main
+                ts = tail if sl.head is not None and self.head_on_tail else main
                 with torch.cuda.stream(ts):
                     if sl.head is not None:
-                        ts.wait_event(ev_sa)
+                        if ts is not main:
+                            ts.wait_event(ev_sa)
                         mark(i - first, "hd0", ts)
                         sl.head.replay()
                     out = _clone(sl.out)
                     # recorded before `post` (e.g. an all_gather) so the group's next fps
                     # replay does not wait for the collective; a later batch of the group
                     # replaces it (same streams, later in their order)
-                    ev_read[s] = ts.record_event() if sl.tail_reads_geometry else ev_sa
+                    ev_read[s].append(ts.record_event() if sl.tail_reads_geometry else ev_sa)
                     if post is not None:
                         out = post(i, out)
                     ev_head[bs] = ts.record_event()
@@ -639,7 +674,7 @@ class GraphedPipeline(PipelinedForward):
         for g in geos[1:]:
             geo.wait_stream(g)
         self._pinned_evs[self._pinned_cur] = geo.record_event()  # uploads read it
-        for st in (geo, main, tail):
+        for st in [geo] + mains + [tail]:
             caller.wait_stream(st)
         return outs
 

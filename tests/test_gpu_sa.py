@@ -399,12 +399,16 @@ def test_graphed_pipeline_multihead_matches_eager(layout):
                                        err_msg="head %d of batch %d" % (k, i))
 
 
-def test_graphed_pipeline_delayed_tail_matches_eager():
+@pytest.mark.parametrize("compute_streams,geometry_streams", [(1, 2), (2, 1), (2, 2)])
+def test_graphed_pipeline_delayed_tail_matches_eager(compute_streams, geometry_streams):
     """A slow tail stream must not let a slot's next fps replay overwrite geometry that the slot's
     head graph still reads: with the group_all split, sa3 (in the head graph) reads sa2's
     centroids, a static output of the fps graph.  `post` runs on the tail stream and sleeps
     there, so every head replay starts late; the geometry streams run ahead as far as the
-    events allow.  The l3 features must still be the eager bits."""
+    events allow.  The l3 features must still be the eager bits.  compute_streams=2: the two
+    batches of a geometry group run on different compute streams, and the group's next fps
+    replay must wait for both; with two geometry streams too the heads run after their sa
+    graph on the compute stream (`post` sleeps there)."""
     from pn2 import heads as H
     from pn2.pipeline import GraphedPipeline
     torch.manual_seed(8)
@@ -422,8 +426,10 @@ def test_graphed_pipeline_delayed_tail_matches_eager():
         torch.cuda._sleep(4_000_000)  # on the tail stream, before the next head replay
         return o
 
-    gp = GraphedPipeline(model, tail=True)
+    gp = GraphedPipeline(model, tail=True, compute_streams=compute_streams,
+                         geometry_streams=geometry_streams)
     assert gp._split_index() == 1  # sa3 (group_all) is in the head graph
+    assert gp.head_on_tail == (compute_streams + geometry_streams < 4)
     torch.manual_seed(17)
     got = [o[1].cpu().numpy() for o in gp.run(xs, post=slow)]
     for i, (g, w) in enumerate(zip(got, want)):
