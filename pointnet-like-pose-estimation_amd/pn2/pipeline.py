@@ -100,14 +100,36 @@ def _masked_stream(device, cus, ncu):
 _XCDS = 8
 
 
+_extra = {}  # device -> (second geometry stream, second compute stream)
+
+
 def _streams(device, geometry_cus):
     key = (device, geometry_cus)
     if key not in _partitions and int(geometry_cus) <= 0:
-        # no partition: three ordinary streams sharing every CU, geometry at high priority
+        # no partition: ordinary streams sharing every CU, geometry at high priority.  A HIP
+        # stream is bound to one of the process's hardware queues at its first command (up to
+        # GPU_MAX_HW_QUEUES = 4 per priority; past that, the least-used one).  Which queue a
+        # pipeline stream lands on changed the throughput by up to 45 % (SSG, rocprofv3
+        # Queue_Id per dispatch, tools/debug/gpipe_events.py): with the default stream's queue
+        # first, the streams first used second and third ran at full speed, while a stream on
+        # the fourth queue fell behind -- the tail stream there took 570-800 us per head
+        # instead of 130-300 (58-65k clouds/s), the second compute stream there cost ~8 %
+        # (97-100k), and a stream first used late (after the captures' streams) shared another
+        # pipeline stream's queue (84-87k).  So the geometry, first compute and tail streams
+        # each run one tiny command here, in that order, and the second compute stream is the
+        # default stream itself, whose queue exists from the start: 103-106k at any slot count.
         dev = torch.device("cuda", device)
         lo, hi = torch.cuda.Stream.priority_range()
-        _partitions[key] = (torch.cuda.Stream(dev, priority=min(lo, hi)), torch.cuda.Stream(dev),
-                            torch.cuda.Stream(dev), ())
+        geo = torch.cuda.Stream(dev, priority=min(lo, hi))
+        geo2 = torch.cuda.Stream(dev, priority=min(lo, hi))
+        main, tail = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        main2 = torch.cuda.default_stream(dev)
+        for st in (geo, main, tail):
+            with torch.cuda.stream(st):
+                torch.zeros(1, device=dev)
+            st.synchronize()
+        _partitions[key] = (geo, main, tail, ())
+        _extra[device] = (geo2, main2)
     if key not in _partitions:
         ncu = _cu_count(device)
         per = max(1, min(int(geometry_cus) // _XCDS, ncu // _XCDS - 1))  # CUs per XCD
@@ -119,26 +141,18 @@ def _streams(device, geometry_cus):
     return _partitions[key][:3]
 
 
-_geo_extra = {}
-
-
 def _extra_geometry_streams(device, n):
-    """n more high-priority streams for GraphedPipeline(geometry_streams=1+n) (shared CUs)."""
-    have = _geo_extra.setdefault(device, [])
-    lo, hi = torch.cuda.Stream.priority_range()
-    while len(have) < n:
-        have.append(torch.cuda.Stream(torch.device("cuda", device), priority=min(lo, hi)))
-    return have[:n]
-
-
-_compute_extra = {}
+    """n (0 or 1) more high-priority streams for GraphedPipeline(geometry_streams=1+n) (shared
+    CUs; created with the others by _streams)."""
+    _streams(device, 0)
+    return [_extra[device][0]][:n]
 
 
 def _extra_compute_stream(device):
-    """A second default-priority compute stream for GraphedPipeline(compute_streams=2)."""
-    if device not in _compute_extra:
-        _compute_extra[device] = torch.cuda.Stream(torch.device("cuda", device))
-    return _compute_extra[device]
+    """The second compute stream for GraphedPipeline(compute_streams=2) (created with the
+    others by _streams)."""
+    _streams(device, 0)
+    return _extra[device][1]
 
 
 def partition(device, geometry_cus):
