@@ -127,6 +127,47 @@ __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const floa
 }
 
 
+// Layer 0's output blocks (layer 1's input) are held as fp32 when the arithmetic is split
+// (NP = 3: 8 VGPRs per block instead of 12 for the three bf16 planes) and split as layer 1
+// consumes them -- layer 1 runs k-outer, so each block is still split exactly once.  At the
+// start of layer 1 the whole input and every accumulator of the layer are live: for the (4, 4)
+// chains that is 96 + 64 VGPRs split, 64 + 64 as fp32.
+struct F8 {
+    float v[8];
+};
+template <int NP> struct HidT { using type = Split; };
+template <> struct HidT<3> { using type = F8; };
+
+template <int NP>
+__device__ __forceinline__ void hidden_epilogue_h(const cfloatx16 &acc, const float *al,
+                                                  const float *be, int t, int h,
+                                                  typename HidT<NP>::type &lo,
+                                                  typename HidT<NP>::type &hi) {
+    if constexpr (NP == 3) {
+        cfloatx4 a4[4], b4[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            a4[m] = *reinterpret_cast<const cfloatx4 *>(al + 32 * t + 8 * m + 4 * h);
+            b4[m] = *reinterpret_cast<const cfloatx4 *>(be + 32 * t + 8 * m + 4 * h);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            lo.v[q] = chain_relu(__builtin_fmaf(acc[q], a4[q >> 2][q & 3], b4[q >> 2][q & 3]));
+            hi.v[q] = chain_relu(__builtin_fmaf(acc[q + 8], a4[2 + (q >> 2)][q & 3], b4[2 + (q >> 2)][q & 3]));
+        }
+    } else {
+        hidden_epilogue<NP>(acc, al, be, t, h, lo, hi);
+    }
+}
+template <int NP>
+__device__ __forceinline__ Split hid_split(const Split &x) { return x; }
+template <int NP>
+__device__ __forceinline__ Split hid_split(const F8 &x) { return splitN<NP>(x.v); }
+__device__ __forceinline__ unsigned hid_dep(const Split &x) {
+    return __builtin_bit_cast(unsigned, __builtin_shufflevector(x.h, x.h, 0, 1));
+}
+__device__ __forceinline__ unsigned hid_dep(const F8 &x) { return __float_as_uint(x.v[0]); }
+
 // Materialise a split pair in registers at this point (see the layer-0 pre-pass loop): keeps
 // the compiler from sinking an epilogue to the pair's last use and holding its inputs live.
 template <int NP>
@@ -135,6 +176,13 @@ __device__ __forceinline__ void pin_pair(Split &a, Split &b) {
         asm volatile("" : "+v"(a.h), "+v"(a.m), "+v"(a.l), "+v"(b.h), "+v"(b.m), "+v"(b.l));
     else
         asm volatile("" : "+v"(a.h), "+v"(b.h));
+}
+template <int NP>
+__device__ __forceinline__ void pin_pair(F8 &a, F8 &b) {
+    asm volatile("" : "+v"(a.v[0]), "+v"(a.v[1]), "+v"(a.v[2]), "+v"(a.v[3]), "+v"(a.v[4]),
+                      "+v"(a.v[5]), "+v"(a.v[6]), "+v"(a.v[7]));
+    asm volatile("" : "+v"(b.v[0]), "+v"(b.v[1]), "+v"(b.v[2]), "+v"(b.v[3]), "+v"(b.v[4]),
+                      "+v"(b.v[5]), "+v"(b.v[6]), "+v"(b.v[7]));
 }
 
 // ---- workgroup weight ring.  A step = one (tile, k-block) of a layer = its three 1 KB plane
@@ -358,7 +406,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         return w;
     };
 
-    Split X1[2 * T0];
+    typename HidT<NP>::type X1[2 * T0];
     if constexpr (KB0M < 0) {
         // ---- layer 0 pre-transformed: acc = z[point] - u[group], already in the transposed
         // accumulator layout (register 4m + i of lane (r, h) = channel 32t + 8m + 4h + i)
@@ -393,8 +441,8 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
                 for (int i = 0; i < 4; ++i) acc[4 * m + i] = zc[m][i] - uc[m][i];
             int zero = 0;  // the BN scale / shift reads of tile t wait for tile t-1 likewise
             asm volatile("" : "+v"(zero) : "v"(dep));
-            hidden_epilogue<NP>(acc, al0 + zero, be0 + zero, t, h, X1[2 * t], X1[2 * t + 1]);
-            dep = __builtin_bit_cast(unsigned, __builtin_shufflevector(X1[2 * t].h, X1[2 * t].h, 0, 1));
+            hidden_epilogue_h<NP>(acc, al0 + zero, be0 + zero, t, h, X1[2 * t], X1[2 * t + 1]);
+            dep = hid_dep(X1[2 * t]);
 #pragma unroll
             for (int m = 0; m < 4; ++m) zc[m] = zn[m], uc[m] = un[m];
             // Materialise tile t's split planes here: otherwise the epilogue of the last tile is
@@ -423,7 +471,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
 #pragma unroll
         for (int t = 0; t < T0; ++t) {
-            hidden_epilogue<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+            hidden_epilogue_h<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
             pin_pair<NP>(X1[2 * t], X1[2 * t + 1]);
         }
     } else {
@@ -450,7 +498,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         for (int st = 0; st < KS - 1; ++st) issue_stage(st);
 #pragma unroll
         for (int t = 0; t < T0; ++t) {
-            hidden_epilogue<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+            hidden_epilogue_h<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
             pin_pair<NP>(X1[2 * t], X1[2 * t + 1]);
         }
     }
@@ -466,9 +514,11 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
 #pragma unroll
-        for (int kb = 0; kb < KB1; ++kb)
+        for (int kb = 0; kb < KB1; ++kb) {
+            const Split xs = hid_split<NP>(X1[kb]);
 #pragma unroll
-            for (int t = 0; t < T1; ++t) acc[t] = mma_wa<NP>(read_w(), X1[kb], acc[t]);
+            for (int t = 0; t < T1; ++t) acc[t] = mma_wa<NP>(read_w(), xs, acc[t]);
+        }
 #pragma unroll
         for (int t = 0; t < T1; ++t) hidden_epilogue<NP>(acc[t], al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
     }

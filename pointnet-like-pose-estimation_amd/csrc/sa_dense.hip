@@ -26,6 +26,26 @@
 
 namespace pn2 {
 
+// Timeline stamps (diagnostic builds only: -DPN2_DENSE_STAMPS, tools/debug/dense_stamps.py):
+// s_memrealtime (100 MHz, chip-wide) of every workgroup of the last launch, wave 0 lane 0:
+// [0] entry, [1 + c] past stage c's barrier (c < 12), [14] main loop done, [15] exit.
+#ifdef PN2_DENSE_STAMPS
+constexpr int kDStampWG = 4096, kDStamps = 16;
+__device__ unsigned long long g_dense_stamps[kDStampWG * kDStamps];
+#define PN2_DSTAMP(i)                                                                           \
+    do {                                                                                        \
+        const unsigned b_ = blockIdx.x + blockIdx.y * gridDim.x;                                \
+        if (threadIdx.x == 0 && b_ < kDStampWG)                                                 \
+            g_dense_stamps[b_ * kDStamps + (i)] = __builtin_amdgcn_s_memrealtime();             \
+    } while (0)
+extern "C" int pn2_debug_dense_stamps(unsigned long long *dst, int64_t n) {
+    const int64_t m = n < (int64_t)kDStampWG * kDStamps ? n : (int64_t)kDStampWG * kDStamps;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dense_stamps), m * 8) == hipSuccess ? 0 : -1;
+}
+#else
+#define PN2_DSTAMP(i) do {} while (0)
+#endif
+
 constexpr int kDW = 4;            // waves per workgroup
 constexpr int kDRows = 32 * kDW;  // rows per workgroup
 constexpr int kKC = 4;            // k-blocks per weight stage
@@ -80,6 +100,7 @@ __device__ __forceinline__ void dma16(const char *src, char *dst) {
 template <int NTC, int NP, bool FAST>
 __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitArgs A) {
     extern __shared__ __attribute__((aligned(16))) char dsm[];
+    PN2_DSTAMP(0);
     constexpr int kFrag = NP * NTC;                  // fragments per k-block
     constexpr int kStage = kKC * kFrag * 1024;       // bytes per weight stage
     const int tid = threadIdx.x;
@@ -151,12 +172,21 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
     auto load_fast = [&](int c, float (&x)[kKC][8]) {
         const int kb0 = c * kKC;
         if (kb0 + kKC <= A.kb) {
+#ifdef PN2_DENSE_DIAG_COALESCED
+            // diagnostic only (wrong results): rows mode reads the same bytes per wave as
+            // whole lines
+            const float *p = A.mode == 0 ? A.rows + (int64_t)(row0 + 32 * wave) * A.rs + 16 * kb0 * 32 + lane * 4
+                                         : lrow + 16 * kb0;
+            const int ks = A.mode == 0 ? 512 : 16, rs_ = A.mode == 0 ? 256 : 8;
+#else
             const float *p = lrow + 16 * kb0;
+            constexpr int ks = 16, rs_ = 8;
+#endif
 #pragma unroll
             for (int k = 0; k < kKC; ++k)
 #pragma unroll
                 for (int run = 0; run < 2; ++run) {
-                    const cfloatx4 q = *reinterpret_cast<const cfloatx4 *>(p + 16 * k + 8 * run);
+                    const cfloatx4 q = *reinterpret_cast<const cfloatx4 *>(p + ks * k + rs_ * run);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) x[k][4 * run + i] = q[i];
                 }
@@ -215,6 +245,7 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
         // whole in LDS and buffer (c+1)&1 is free again
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         __syncthreads();
+        if (c < 12) PN2_DSTAMP(1 + c);
         if (c + 1 < nst) {
             if constexpr (FAST) {
                 load_fast(c + 1, xn);
@@ -225,13 +256,51 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
             issue_stage(c + 1);
         }
         const char *buf = stages + (c & 1) * kStage;
+        if (c * kKC + kKC <= A.kb) {
+            // a whole stage, branch-free and software-pipelined: block k+1's weight fragments
+            // are read from LDS and its rows split while block k's MFMAs run (the compiler
+            // alone issued each fragment read just before its MFMA, behind a wait, and split a
+            // block only after the previous block's MFMAs)
+            Split w[NTC];
 #pragma unroll
-        for (int k = 0; k < kKC; ++k) {
-            if (c * kKC + k < A.kb) {
-                const Split xs = splitN<NP>(xc[k]);
+            for (int i = 0; i < NTC; ++i) w[i] = ring_readN<NP>(buf + NP * i * 1024, lane);
+            Split xs = splitN<NP>(xc[0]);
 #pragma unroll
-                for (int i = 0; i < NTC; ++i)
-                    acc[i] = mma_wb<NP>(xs, ring_readN<NP>(buf + (k * kFrag + NP * i) * 1024, lane), acc[i]);
+            for (int k = 0; k < kKC; ++k) {
+                Split wn[NTC], xsn;
+                if (k + 1 < kKC) {
+#pragma unroll
+                    for (int i = 0; i < NTC; ++i)
+                        wn[i] = ring_readN<NP>(buf + ((k + 1) * kFrag + NP * i) * 1024, lane);
+                    xsn = splitN<NP>(xc[k + 1]);
+                }
+#pragma unroll
+                for (int i = 0; i < NTC; ++i) acc[i] = mma_wb<NP>(xs, w[i], acc[i]);
+                if (k + 1 < kKC) {
+#ifndef PN2_DENSE_NO_SGB
+                    // order: the next block's fragment reads first, then each MFMA followed
+                    // by a few of the next block's split instructions
+                    __builtin_amdgcn_sched_group_barrier(0x100, NP * NTC, 0);
+#pragma unroll
+                    for (int m = 0; m < NP * 2 * NTC; ++m) {
+                        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x2, 4, 0);
+                    }
+#endif
+#pragma unroll
+                    for (int i = 0; i < NTC; ++i) w[i] = wn[i];
+                    xs = xsn;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kKC; ++k) {
+                if (c * kKC + k < A.kb) {
+                    const Split xs = splitN<NP>(xc[k]);
+#pragma unroll
+                    for (int i = 0; i < NTC; ++i)
+                        acc[i] = mma_wb<NP>(xs, ring_readN<NP>(buf + (k * kFrag + NP * i) * 1024, lane), acc[i]);
+                }
             }
         }
     };
@@ -243,6 +312,7 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
         step(c, xa, xb);
         if (c + 1 < nst) step(c + 1, xb, xa);
     }
+    PN2_DSTAMP(14);
 
     // ---- epilogue: lane = output column, register q = row (q&3) + 8(q>>2) + 4h of the slab
     const int slab_row = row0 + 32 * wave;
@@ -332,6 +402,7 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
                     A.norelu ? funkey(__float_as_uint(opool[e])) : opool[e];
         }
     }
+    PN2_DSTAMP(15);
 }
 
 template <int NTC, int NP>
@@ -342,6 +413,16 @@ static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
     const size_t lds = (size_t)2 * kKC * NP * NTC * 1024 +
                        (A.pool_mode == 1 ? (size_t)(kDRows / A.K) * 32 * NTC * 4 : 0);
     dim3 grid((unsigned)((A.M + kDRows - 1) / kDRows), (unsigned)(A.tiles / NTC));
+    if (lds > 64 * 1024) {  // NTC = 4: two 48 KB weight stages (one-time, idempotent)
+        static const hipError_t a1 = hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&dense_split_kernel<NTC, NP, true>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        static const hipError_t a2 = hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&dense_split_kernel<NTC, NP, false>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)a1;
+        (void)a2;
+    }
     if (fast) hipLaunchKernelGGL((dense_split_kernel<NTC, NP, true>), grid, dim3(64 * kDW), lds, st, A);
     else hipLaunchKernelGGL((dense_split_kernel<NTC, NP, false>), grid, dim3(64 * kDW), lds, st, A);
     PN2_LAUNCH_CHECK("dense_split_kernel");
@@ -349,9 +430,16 @@ static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
 }
 
 static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
-    // two output tiles per wave when that still leaves >= 2 workgroups per CU
+    // the widest tile (NTC 32-column tiles per wave) that still leaves min_wg workgroups
     const int64_t rowblocks = (A.M + kDRows - 1) / kDRows;
-    const int ntc = (A.tiles % 2 == 0 && rowblocks * (A.tiles / 2) >= 512) ? 2 : 1;
+    static const int64_t min_wg = getenv("PN2_DENSE_MINWG") ? atol(getenv("PN2_DENSE_MINWG")) : 512;
+    static const int max_ntc = getenv("PN2_DENSE_MAXNTC") ? atoi(getenv("PN2_DENSE_MAXNTC")) : 2;
+    int ntc = 1;
+    for (int t = max_ntc; t > 1; t /= 2)
+        if (A.tiles % t == 0 && rowblocks * (A.tiles / t) >= min_wg) {
+            ntc = t;
+            break;
+        }
     if (A.pool) {
         if (A.K == 8 || A.K == 16) A.pool_mode = 0;
         else if (A.K % 32 == 0 && kDRows % A.K == 0) A.pool_mode = 1;
@@ -365,8 +453,10 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
         }
     }
     int rc;
-    if (np == 1) rc = ntc == 2 ? launch_dense_split<2, 1>(A, st) : launch_dense_split<1, 1>(A, st);
-    else rc = ntc == 2 ? launch_dense_split<2, 3>(A, st) : launch_dense_split<1, 3>(A, st);
+    if (np == 1) rc = ntc == 4 ? launch_dense_split<4, 1>(A, st) : ntc == 2 ? launch_dense_split<2, 1>(A, st)
+                                                                      : launch_dense_split<1, 1>(A, st);
+    else rc = ntc == 4 ? launch_dense_split<4, 3>(A, st) : ntc == 2 ? launch_dense_split<2, 3>(A, st)
+                                                           : launch_dense_split<1, 3>(A, st);
     if (rc == PN2_OK && A.pool && A.pool_mode == 2 && A.norelu) {  // keys -> floats
         const int64_t G = A.M / A.K, cols = 32 * (int64_t)A.tiles;
         hipLaunchKernelGGL(unkey_kernel, dim3((unsigned)((G * cols + 255) / 256)), dim3(256), 0, st,

@@ -32,9 +32,10 @@ cases.randomize_bn(model, 8)
 model = model.to(DEV)
 x = cases.cloud(kind, B, N, 90).permute(0, 2, 1).contiguous().to(DEV)
 ex = [(torch.zeros(B, 3, device=DEV),)] if pose else None
-gp = GraphedPipeline(model, nslots=int(os.environ.get("SLOTS", "6")),
-                     geometry_streams=int(os.environ.get("GEOS", "2")),
-                     geometry_batches=int(os.environ.get("GB", "2")))
+gp = GraphedPipeline(model, nslots=int(os.environ.get("SLOTS", "8")),
+                     geometry_streams=int(os.environ.get("GEOS", "1")),
+                     geometry_batches=int(os.environ.get("GB", "2")),
+                     compute_streams=int(os.environ["CS"]) if "CS" in os.environ else None)
 K = 100
 gp.run([x] * 3, None if ex is None else ex * 3)
 torch.cuda.synchronize()
