@@ -97,8 +97,9 @@ __device__ __forceinline__ void dma16(const char *src, char *dst) {
     __builtin_amdgcn_global_load_lds(src, (lds_void *)dst, 16, 0, 0);
 }
 
-template <int NTC, int NP, bool FAST>
-__global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitArgs A) {
+template <int NTC, int NP, bool FAST, int NW>
+__global__ __launch_bounds__(64 * NW) void dense_split_kernel(const DenseSplitArgs A) {
+    constexpr int kDW = NW, kDRows = 32 * NW;  // waves, rows per workgroup
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     PN2_DSTAMP(0);
     constexpr int kFrag = NP * NTC;                  // fragments per k-block
@@ -257,40 +258,15 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
         }
         const char *buf = stages + (c & 1) * kStage;
         if (c * kKC + kKC <= A.kb) {
-            // a whole stage, branch-free and software-pipelined: block k+1's weight fragments
-            // are read from LDS and its rows split while block k's MFMAs run (the compiler
-            // alone issued each fragment read just before its MFMA, behind a wait, and split a
-            // block only after the previous block's MFMAs)
-            Split w[NTC];
-#pragma unroll
-            for (int i = 0; i < NTC; ++i) w[i] = ring_readN<NP>(buf + NP * i * 1024, lane);
-            Split xs = splitN<NP>(xc[0]);
+            // a whole stage, branch-free (one basic block for the scheduler).  Reading block
+            // k+1's fragments and splitting its rows under block k's MFMAs by hand
+            // (sched_group_barrier) measured no faster, and cost registers.
 #pragma unroll
             for (int k = 0; k < kKC; ++k) {
-                Split wn[NTC], xsn;
-                if (k + 1 < kKC) {
+                const Split xs = splitN<NP>(xc[k]);
 #pragma unroll
-                    for (int i = 0; i < NTC; ++i)
-                        wn[i] = ring_readN<NP>(buf + ((k + 1) * kFrag + NP * i) * 1024, lane);
-                    xsn = splitN<NP>(xc[k + 1]);
-                }
-#pragma unroll
-                for (int i = 0; i < NTC; ++i) acc[i] = mma_wb<NP>(xs, w[i], acc[i]);
-                if (k + 1 < kKC) {
-#ifndef PN2_DENSE_NO_SGB
-                    // order: the next block's fragment reads first, then each MFMA followed
-                    // by a few of the next block's split instructions
-                    __builtin_amdgcn_sched_group_barrier(0x100, NP * NTC, 0);
-#pragma unroll
-                    for (int m = 0; m < NP * 2 * NTC; ++m) {
-                        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x2, 4, 0);
-                    }
-#endif
-#pragma unroll
-                    for (int i = 0; i < NTC; ++i) w[i] = wn[i];
-                    xs = xsn;
-                }
+                for (int i = 0; i < NTC; ++i)
+                    acc[i] = mma_wb<NP>(xs, ring_readN<NP>(buf + (k * kFrag + NP * i) * 1024, lane), acc[i]);
             }
         } else {
 #pragma unroll
@@ -405,8 +381,9 @@ __global__ __launch_bounds__(64 * kDW) void dense_split_kernel(const DenseSplitA
     PN2_DSTAMP(15);
 }
 
-template <int NTC, int NP>
+template <int NTC, int NP, int NW = 4>
 static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
+    constexpr int kDW = NW, kDRows = 32 * NW;
     // every k-block after the first stage is one contiguous 16-channel run of the row
     const bool fast = A.vec && (A.mode == 0 ? A.cin % 16 == 0 && A.kb * 16 == A.cin
                                             : A.feat && A.D > 0 && A.D % 16 == 0 && A.kb == 1 + A.D / 16);
@@ -415,22 +392,29 @@ static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
     dim3 grid((unsigned)((A.M + kDRows - 1) / kDRows), (unsigned)(A.tiles / NTC));
     if (lds > 64 * 1024) {  // NTC = 4: two 48 KB weight stages (one-time, idempotent)
         static const hipError_t a1 = hipFuncSetAttribute(
-            reinterpret_cast<const void *>(&dense_split_kernel<NTC, NP, true>),
+            reinterpret_cast<const void *>(&dense_split_kernel<NTC, NP, true, NW>),
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         static const hipError_t a2 = hipFuncSetAttribute(
-            reinterpret_cast<const void *>(&dense_split_kernel<NTC, NP, false>),
+            reinterpret_cast<const void *>(&dense_split_kernel<NTC, NP, false, NW>),
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)a1;
         (void)a2;
     }
-    if (fast) hipLaunchKernelGGL((dense_split_kernel<NTC, NP, true>), grid, dim3(64 * kDW), lds, st, A);
-    else hipLaunchKernelGGL((dense_split_kernel<NTC, NP, false>), grid, dim3(64 * kDW), lds, st, A);
+    if (fast) hipLaunchKernelGGL((dense_split_kernel<NTC, NP, true, NW>), grid, dim3(64 * kDW), lds, st, A);
+    else hipLaunchKernelGGL((dense_split_kernel<NTC, NP, false, NW>), grid, dim3(64 * kDW), lds, st, A);
     PN2_LAUNCH_CHECK("dense_split_kernel");
     return PN2_OK;
 }
 
 static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
-    // the widest tile (NTC 32-column tiles per wave) that still leaves min_wg workgroups
+    // Large layers (e.g. translation_ssg's group_all over B*512 rows) take 256 x 128 tiles (8
+    // waves of 32 rows x 4 column tiles): the 128 x 64 tile re-reads its A rows once per 64
+    // output columns and its weights once per 128 rows, and at these sizes that L2 -> CU
+    // stream, not the MFMA, was the bound.  Only when they still leave wide_min workgroups.
+    static const int64_t wide_min = getenv("PN2_DENSE_WIDE_MINWG") ? atol(getenv("PN2_DENSE_WIDE_MINWG")) : 512;
+    const bool wide = A.tiles % 4 == 0 && (A.M + 255) / 256 * (A.tiles / 4) >= wide_min;
+    const int64_t kRowsSel = wide ? 256 : kDRows;
+    // otherwise the widest tile (NTC 32-column tiles per wave) that still leaves min_wg workgroups
     const int64_t rowblocks = (A.M + kDRows - 1) / kDRows;
     static const int64_t min_wg = getenv("PN2_DENSE_MINWG") ? atol(getenv("PN2_DENSE_MINWG")) : 512;
     static const int max_ntc = getenv("PN2_DENSE_MAXNTC") ? atoi(getenv("PN2_DENSE_MAXNTC")) : 2;
@@ -442,7 +426,7 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
         }
     if (A.pool) {
         if (A.K == 8 || A.K == 16) A.pool_mode = 0;
-        else if (A.K % 32 == 0 && kDRows % A.K == 0) A.pool_mode = 1;
+        else if (A.K % 32 == 0 && kRowsSel % A.K == 0) A.pool_mode = 1;
         else A.pool_mode = 2;
         if (A.pool_mode == 2) {
             const int64_t G = A.M / A.K, cols = 32 * (int64_t)A.tiles;
@@ -453,7 +437,8 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
         }
     }
     int rc;
-    if (np == 1) rc = ntc == 4 ? launch_dense_split<4, 1>(A, st) : ntc == 2 ? launch_dense_split<2, 1>(A, st)
+    if (wide) rc = np == 1 ? launch_dense_split<4, 1, 8>(A, st) : launch_dense_split<4, 3, 8>(A, st);
+    else if (np == 1) rc = ntc == 4 ? launch_dense_split<4, 1>(A, st) : ntc == 2 ? launch_dense_split<2, 1>(A, st)
                                                                       : launch_dense_split<1, 1>(A, st);
     else rc = ntc == 4 ? launch_dense_split<4, 3>(A, st) : ntc == 2 ? launch_dense_split<2, 3>(A, st)
                                                            : launch_dense_split<1, 3>(A, st);

@@ -1,7 +1,8 @@
 """Per-workgroup timeline of the dense layer kernel (diagnostic build,
 tools/debug/build_dense_stamps.sh): PN2_LIB=.../pn2/var/dstamps.so python tools/debug/dense_stamps.py
 Runs one eager SSG B=32 N=1024 forward after warm-up; the last dense launch of it is sa3's
-512 -> 1024 layer (group_all, pooled over the 128 points of a cloud).  Prints the spread of
+512 -> 1024 layer (group_all, pooled over the 128 points of a cloud); CONFIG=pose: translation_ssg's
+sa2 512 -> 1024 layer at B=64 (GRID=1024 wide tiles, NST=8).  Prints the spread of
 workgroup start times, percentiles of the prologue (entry -> stage 0 landed), of each stage
 (barrier to barrier), of the epilogue, and of the workgroup lifetime."""
 import ctypes
@@ -23,15 +24,20 @@ fn = _lib.load().pn2_debug_dense_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
 NW, NS = 4096, 16
 torch.manual_seed(8)
-model = H.ClsSSG().eval()
+pose = os.environ.get("CONFIG", "ssg") == "pose"  # translation_ssg B=64 N=2048: group_all over 32768 rows
+model = H.TranslationSSG().eval() if pose else H.ClsSSG().eval()
 cases.randomize_bn(model, 8)
 model = model.to(DEV)
-x = cases.cloud("uniform3", 32, 1024, 90).permute(0, 2, 1).contiguous().to(DEV)
+if pose:
+    x = cases.cloud("onehot10", 64, 2048, 90).permute(0, 2, 1).contiguous().to(DEV)
+    args = (x, torch.zeros(64, 3, device=DEV))
+else:
+    args = (cases.cloud("uniform3", 32, 1024, 90).permute(0, 2, 1).contiguous().to(DEV),)
 with torch.no_grad():
     for _ in range(5):
-        model(x)
+        model(*args)
     torch.cuda.synchronize()
-    model(x)
+    model(*args)
 torch.cuda.synchronize()
 a = np.zeros(NW * NS, np.uint64)
 assert fn(a.ctypes.data, a.size) == 0
