@@ -66,6 +66,10 @@ STRONG = {"pose"}
 # MLP arithmetic per config: BASELINE config 5 (stress) asks for features/MLP in bf16, the
 # others are the reference's fp32
 DEFAULT_PRECISION = {"stress": "bf16"}
+# Geometry streams per config (graphed pipeline): STRESS's N=16384 FPS (~1 ms per group of two
+# batches) needs two geometry streams (116k vs 108-111k clouds/s with one); the others are
+# faster with one geometry stream and a tail stream for the heads.
+DEFAULT_GEOMETRY_STREAMS = {"stress": 2}
 
 
 def parse():
@@ -94,8 +98,9 @@ def parse():
     ap.add_argument("--geometry-batches", type=int, default=2,
                     help="graphed pipeline: consecutive batches whose geometry (FPS + ball "
                          "queries) runs as one replay over their clouds side by side")
-    ap.add_argument("--geometry-streams", type=int, default=1,
-                    help="graphed pipeline: 2 = consecutive batches' FPS chains on two streams")
+    ap.add_argument("--geometry-streams", type=int, default=None,
+                    help="graphed pipeline: 2 = consecutive groups' FPS chains on two streams "
+                         "(default 2 for --config stress, else 1)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="plain eager steps (default for single-head configs: pn2.pipeline)")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default=None,
@@ -329,7 +334,8 @@ def main():
         if not a.eager_pipeline:
             pf = GraphedPipeline(pmodel, geometry_cus=a.geometry_cus,
                                  tail=not a.no_tail, nslots=a.slots,
-                                 geometry_streams=a.geometry_streams,
+                                 geometry_streams=(a.geometry_streams if a.geometry_streams is not None
+                                                   else DEFAULT_GEOMETRY_STREAMS.get(a.config, 1)),
                                  geometry_batches=a.geometry_batches,
                                  compute_streams=a.compute_streams)
         else:
@@ -445,7 +451,9 @@ def main():
                            " on %d dedicated CUs" % a.geometry_cus if a.geometry_cus > 0
                            else "s sharing all CUs") + (
                            "; geometry of %d batches per replay" % a.geometry_batches +
-                           ("; %d compute streams" % pf.compute_streams)
+                           ("; %d compute + %d geometry streams%s" % (
+                               pf.compute_streams, pf.geometry_streams,
+                               "" if pf.head_on_tail else ", heads on the compute streams"))
                            if not a.eager_pipeline else "")
                        if pipelined else "eager"),
             "eager_value": round(eager_value, 2),

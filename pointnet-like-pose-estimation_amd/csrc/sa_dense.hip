@@ -98,7 +98,8 @@ __device__ __forceinline__ void dma16(const char *src, char *dst) {
 }
 
 template <int NTC, int NP, bool FAST, int NW>
-__global__ __launch_bounds__(64 * NW) void dense_split_kernel(const DenseSplitArgs A) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 4 ? (NTC == 1 ? 4 : NTC == 2 ? 3 : 1) : 1)))
+void dense_split_kernel(const DenseSplitArgs A) {
     constexpr int kDW = NW, kDRows = 32 * NW;  // waves, rows per workgroup
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     PN2_DSTAMP(0);
