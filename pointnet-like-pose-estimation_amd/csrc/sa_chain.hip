@@ -33,6 +33,8 @@
 #include "pn2_internal.h"
 #include "split_bf16.h"
 
+#include <algorithm>
+
 #include <cstdlib>
 #include <cstring>
 
@@ -74,6 +76,11 @@ struct ChainArgs {
     const int *cunits;
     const int2 *cdesc;
     int wpc;  // workgroups per cloud
+    // compact: LDS pool rows (groups of a workgroup pooled in LDS; a group past them is merged
+    // straight into its output row by atomicMax -- compact_scan_kernel zeroed that row) and the
+    // weight ring's stage count (2 or 3)
+    int pool_rows;
+    int ks;
 };
 
 // Timeline stamps (diagnostic builds only: -DPN2_CHAIN_STAMPS, tools/debug/chain_stamps.py):
@@ -272,7 +279,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         c_flags = d.y >> 8;
     }
     // groups per workgroup of the LDS pool (pool_mode 1; compact: up to one per unit)
-    const int gpb = compact ? kUnitsPerWG : kChainRows / A.K;
+    const int gpb = compact ? A.pool_rows : kChainRows / A.K;
 
     // ---- this lane's row: (group g, batch b, point n)
     unsigned g;
@@ -548,8 +555,13 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             float smx = 0.f, smn = 0.f;
             int sg = -1;
             auto flush = [&]() {
-                if (sg >= 0 && h == 0)
-                    atomicMax(&cpool[sg * coutL + col], __float_as_uint(fin(smx, smn)));
+                if (sg >= 0 && h == 0) {
+                    if (sg < gpb)
+                        atomicMax(&cpool[sg * coutL + col], __float_as_uint(fin(smx, smn)));
+                    else  // past the pool (rare): the row was zeroed by the scan
+                        atomicMax(reinterpret_cast<unsigned *>(A.out + (int64_t)(c_g0 + (unsigned)sg) * A.ostride + col),
+                                  __float_as_uint(fin(smx, smn)));
+                }
             };
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -620,7 +632,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         __syncthreads();
         // a group shared with the neighbouring workgroup is merged by atomicMax into its row
         // (zeroed by compact_scan_kernel); the others are stored
-        for (int e = tid; e < c_ng * coutL; e += 64 * kChainWaves) {
+        for (int e = tid; e < min(c_ng, gpb) * coutL; e += 64 * kChainWaves) {
             const int gl = e / coutL, c = e - gl * coutL;
             float *o = A.out + (int64_t)(c_g0 + (unsigned)gl) * A.ostride + c;
             if ((gl == 0 && (c_flags & 1)) || (gl == c_ng - 1 && (c_flags & 2)))
@@ -730,7 +742,7 @@ constexpr int kScanThreads = 1024;
 
 __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
     const int *__restrict__ cnt, int S, int K, int wpc, int *__restrict__ units,
-    int2 *__restrict__ desc, float *__restrict__ out, int64_t ostride, int cout) {
+    int2 *__restrict__ desc, float *__restrict__ out, int64_t ostride, int cout, int prow) {
     extern __shared__ int ssm[];
     int *st = ssm;            // [S] units of group s, then its first unit
     int *strad = st + S;      // [S] groups to zero
@@ -770,11 +782,18 @@ __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
         run += u;
     }
     __syncthreads();
-    // the first group of every workgroup (the one holding unit 16w) and the groups that span two
+    // the first group of every workgroup (the one holding unit 16w)
     for (int i = tid; i < S; i += kScanThreads) {
         const int s0 = st[i] >> 8, en = s0 + (st[i] & 255) - 1;
         for (int w = (s0 + kUnitsPerWG - 1) / kUnitsPerWG; w * kUnitsPerWG <= en; ++w) glo[w] = i;
-        if (s0 / kUnitsPerWG != en / kUnitsPerWG) strad[atomicAdd(&wsum[16], 1)] = i;
+    }
+    __syncthreads();
+    // rows to zero: groups that span two workgroups, and groups past the pool rows of the
+    // workgroup holding their first unit (both merged by atomicMax)
+    for (int i = tid; i < S; i += kScanThreads) {
+        const int s0 = st[i] >> 8, en = s0 + (st[i] & 255) - 1;
+        if (s0 / kUnitsPerWG != en / kUnitsPerWG || i - glo[s0 / kUnitsPerWG] >= prow)
+            strad[atomicAdd(&wsum[16], 1)] = i;
     }
     __syncthreads();
     for (int w = tid; w < wpc; w += kScanThreads) {
@@ -837,14 +856,9 @@ extern "C" int pn2_debug_chain_stamps(unsigned long long *dst, int64_t n) {
 }
 #endif
 
-static int compact_stages() {
-    const char *e = getenv("PN2_COMPACT_KS");
-    return (e && strcmp(e, "3") == 0) ? 3 : 2;
-}
-
 template <int T0, int T1, int KB0M, int NP>
 static int launch_chain_sig(const ChainArgs &A, unsigned grid, size_t lds, hipStream_t st) {
-    if (A.pool_mode == 3 && compact_stages() == 2)
+    if (A.pool_mode == 3 && A.ks == 2)
         hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP, 2>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
     else
         hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP, kStages>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
@@ -978,6 +992,24 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         KB0M = -1;
     }
     const int wpc = compact ? (int)compact_wpc(s) : 0;
+    // Compact launches: the weight ring's depth against the LDS group pool.  With the full
+    // 16-row pool a 3-stage ring cost a workgroup per CU (SSG sa2: 3 -> 2 live per CU, 114 ->
+    // 130 us, although each workgroup lived 36 us instead of 45: tools/debug/chain_stamps.py).
+    // An 8-row pool (groups past it merge through HBM atomics into rows the scan zeroed) keeps
+    // 3 per CU with 3 stages -- measured 117.8 vs 114.2 us, so the default stays 2 stages and
+    // 16 rows; PN2_COMPACT_KS=3 selects the 3-stage ring with the 8-row pool when it keeps the
+    // workgroups per CU the registers allow (A/B, and the tests of the overflow path).
+    int cks = 2, cprow = kUnitsPerWG;
+    if (compact && getenv("PN2_COMPACT_KS") && getenv("PN2_COMPACT_KS")[0] == '3') {
+        const int64_t cL = layers[2].cout;
+        const size_t bnb = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + cL) + 32;
+        const size_t sb = np == 3 ? stage_bytes<3>() : stage_bytes<1>();
+        const int occ_v = T1 >= 4 ? 3 : T1 == 3 ? 4 : 5;  // workgroups per CU the VGPRs allow
+        auto wgs = [&](int ks, int prow) {
+            return std::min<int64_t>(occ_v, (int64_t)(160 * 1024) / (int64_t)(prow * cL * 4 + bnb + ks * sb));
+        };
+        if (wgs(3, 8) >= wgs(2, kUnitsPerWG)) cks = 3, cprow = 8;
+    }
     int *cunits = nullptr;
     int2 *cdesc = nullptr;
     if (compact) {
@@ -990,7 +1022,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         (void)attr;
         hipLaunchKernelGGL(compact_scan_kernel, dim3((unsigned)s.B), dim3(kScanThreads), slds, st,
                            s.cnt, (int)s.S, (int)s.K, wpc, cunits, cdesc, out, ostride,
-                           (int)layers[2].cout);
+                           (int)layers[2].cout, cprow);
         PN2_LAUNCH_CHECK("compact_scan_kernel");
     }
     ChainArgs A;
@@ -1023,7 +1055,9 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     size_t lds = 0;
     if (compact) {
         A.pool_mode = 3;
-        lds = (size_t)kUnitsPerWG * coutL * 4;
+        A.pool_rows = cprow;
+        A.ks = cks;
+        lds = (size_t)cprow * coutL * 4;
     } else if (K == 8 || K == 16 || K == 32) {
         A.pool_mode = 0;
     } else if (kChainRows % K == 0) {
@@ -1045,7 +1079,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     A.lds_bn = (int)((lds + 15) / 16 * 16);
     const size_t bn_bytes = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + coutL);
     A.lds_ring = (int)((A.lds_bn + bn_bytes + 15) / 16 * 16);
-    lds = (size_t)A.lds_ring + (size_t)(compact ? compact_stages() : kStages) * (np == 3 ? stage_bytes<3>() : stage_bytes<1>());
+    lds = (size_t)A.lds_ring + (size_t)(compact ? cks : kStages) * (np == 3 ? stage_bytes<3>() : stage_bytes<1>());
     int rc = PN2_EUNSUPPORTED;
 #define PN2_CHAIN_GO(a, b, c)                                                             \
     if (T0 == a && T1 == b && KB0M == c)                                                  \

@@ -132,6 +132,11 @@ COMPACT = [
     (3, 0, 128, 32, 512, 0.5, [64, 64, 128], False),      # up to 16 units per group
     (3, 13, 16, 64, 512, 0.1, [32, 32, 64], True),        # MSG row order, unaligned features
     (10, 0, 32, 256, 2048, 0.2, [64, 64, 128], False),    # pose layout
+    # SSG sa2 shapes with small balls: one-unit groups, 16 groups per workgroup -- past the
+    # 8-row LDS pool of the 3-stage-ring launch (PN2_COMPACT_KS=3; merged by HBM atomics into
+    # zeroed rows)
+    (3, 128, 64, 128, 512, 0.05, [128, 128, 256], False),
+    (3, 128, 64, 128, 512, 0.15, [128, 128, 256], False),  # a mix of pooled and overflow groups
 ]
 
 
@@ -142,9 +147,12 @@ def test_compact_neighbourhoods_bit_exact(case, prec, monkeypatch):
     neighbour dropped) gives the bits of the full K rows per group: every row's MLP is
     computed the same way, and the max is the same without repeats.  Covers K % 8 != 0, groups
     spanning two workgroups (merged by atomicMax into rows the scan zeroed), up to 16 units per
-    group, MSG, the pose layout, and bf16; the fp32 result also against the float64 oracle."""
+    group, MSG, the pose layout, groups past the LDS pool rows, and bf16; the fp32 result also
+    against the float64 oracle."""
     import pn2
     C, D, K, S, N, radius, mlp, msg = COMPACT[case]
+    if case >= 7:
+        monkeypatch.setenv("PN2_COMPACT_KS", "3")
     B = 3
     pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 500 + case)
     gen = torch.Generator().manual_seed(600 + case)
