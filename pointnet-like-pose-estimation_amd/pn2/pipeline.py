@@ -680,10 +680,20 @@ class GraphedPipeline(PipelinedForward):
                     # replay does not wait for the collective; a later batch of the group
                     # replaces it (same streams, later in their order)
                     ev_read[s].append(ts.record_event() if sl.tail_reads_geometry else ev_sa)
-                    if post is not None:
+                    if post is not None and ts is tail:
                         out = post(i, out)
                     ev_head[bs] = ts.record_event()
                     mark(i - first, "hd1", ts)
+                if post is not None and ts is not tail:
+                    # heads on the compute streams: `post` (e.g. the logits' all_gather) still
+                    # runs on one stream in batch order, so every rank's collectives execute in
+                    # the order they were issued
+                    tail.wait_stream(ts)
+                    with torch.cuda.stream(tail):
+                        for t in (out if isinstance(out, (tuple, list)) else (out,)):
+                            if isinstance(t, torch.Tensor):
+                                t.record_stream(tail)
+                        out = post(i, out)
                 outs.append(out)
         for g in geos[1:]:
             geo.wait_stream(g)

@@ -408,7 +408,8 @@ def test_graphed_pipeline_delayed_tail_matches_eager(compute_streams, geometry_s
     events allow.  The l3 features must still be the eager bits.  compute_streams=2: the two
     batches of a geometry group run on different compute streams, and the group's next fps
     replay must wait for both; with two geometry streams too the heads run after their sa
-    graph on the compute stream (`post` sleeps there)."""
+    graph on the compute stream and `post` still on the tail stream, in batch order (the
+    collective order every rank must keep)."""
     from pn2 import heads as H
     from pn2.pipeline import GraphedPipeline
     torch.manual_seed(8)
