@@ -30,14 +30,15 @@ from .pointnet_utils import linear_bn
 
 class _FCHead(nn.Module):
     """fc1/bn1/relu/drop -> fc2/bn2/relu/drop -> fc3, shared by every head.  Eval without
-    autograd: each fc + bn folded into one GEMM with the ReLU (pn2.pointnet_utils.linear_bn;
-    dropout is the identity in eval)."""
+    autograd: each fc + bn folded into one GEMM with the ReLU, and fc3, on pn2's row kernel
+    (pn2.pointnet_utils.linear_bn; dropout is the identity in eval)."""
 
     def _fc(self, x):
         if not _needs_autograd(self, x):
             x = linear_bn(x, self.fc1, self.bn1, self._fc_cache.setdefault(1, {}))
             x = linear_bn(x, self.fc2, self.bn2, self._fc_cache.setdefault(2, {}))
-            return self.fc3(x)
+            # fc3 on the same row kernel (a library GEMM launch for 256 -> 3 / 7 took ~5 us)
+            return linear_bn(x, self.fc3, None, self._fc_cache.setdefault(3, {}), relu=False)
         x = self.drop(F.relu(self.bn1(self.fc1(x))))
         x = self.drop(F.relu(self.bn2(self.fc2(x))))
         return self.fc3(x)

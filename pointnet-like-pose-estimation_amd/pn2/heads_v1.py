@@ -108,10 +108,12 @@ class PointNetCls(nn.Module):
         if not _needs_autograd(self, x):  # eval: fc + bn folded (dropout is the identity)
             x = linear_bn(x, self.fc1, self.bn1, self._fc_cache.setdefault(1, {}))
             x = linear_bn(x, self.fc2, self.bn2, self._fc_cache.setdefault(2, {}))
+            x = linear_bn(x, self.fc3, None, self._fc_cache.setdefault(3, {}), relu=False)
         else:
             x = F.relu(self.bn1(self.fc1(x)))
             x = F.relu(self.bn2(self.dropout(self.fc2(x))))
-        x = F.log_softmax(self.fc3(x), dim=1)
+            x = self.fc3(x)
+        x = F.log_softmax(x, dim=1)
         return x, trans_feat, x.data.max(1)[1]
 
 
