@@ -996,11 +996,11 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     // 16-row pool a 3-stage ring cost a workgroup per CU (SSG sa2: 3 -> 2 live per CU, 114 ->
     // 130 us, although each workgroup lived 36 us instead of 45: tools/debug/chain_stamps.py).
     // An 8-row pool (groups past it merge through HBM atomics into rows the scan zeroed) keeps
-    // 3 per CU with 3 stages -- measured 117.8 vs 114.2 us, so the default stays 2 stages and
-    // 16 rows; PN2_COMPACT_KS=3 selects the 3-stage ring with the 8-row pool when it keeps the
+    // 3 per CU with 3 stages -- measured 117.8 vs 114.2 us, so the default stays 2 stages;
+    // PN2_COMPACT_KS=3 selects the 3-stage ring with the 8-row pool when it keeps the
     // workgroups per CU the registers allow (A/B, and the tests of the overflow path).
     int cks = 2, cprow = kUnitsPerWG;
-    if (compact && getenv("PN2_COMPACT_KS") && getenv("PN2_COMPACT_KS")[0] == '3') {
+    if (compact) {
         const int64_t cL = layers[2].cout;
         const size_t bnb = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + cL) + 32;
         const size_t sb = np == 3 ? stage_bytes<3>() : stage_bytes<1>();
@@ -1008,7 +1008,13 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         auto wgs = [&](int ks, int prow) {
             return std::min<int64_t>(occ_v, (int64_t)(160 * 1024) / (int64_t)(prow * cL * 4 + bnb + ks * sb));
         };
-        if (wgs(3, 8) >= wgs(2, kUnitsPerWG)) cks = 3, cprow = 8;
+        // an 8-row pool when it buys a workgroup per CU (SSG sa1: 4 -> 5 per CU, 62.4 -> 59.9
+        // us; its many small groups past the 8th of a workgroup merge through HBM atomics)
+        if (wgs(2, 8) > wgs(2, kUnitsPerWG)) cprow = 8;
+        if (const char *e = getenv("PN2_COMPACT_POOL"))  // A/B override of the pool rows
+            cprow = std::max(1, std::min<int>(kUnitsPerWG, atoi(e)));
+        if (getenv("PN2_COMPACT_KS") && getenv("PN2_COMPACT_KS")[0] == '3' && wgs(3, 8) >= wgs(2, kUnitsPerWG))
+            cks = 3, cprow = 8;
     }
     int *cunits = nullptr;
     int2 *cdesc = nullptr;
