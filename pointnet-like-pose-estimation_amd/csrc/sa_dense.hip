@@ -412,7 +412,7 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
     // waves of 32 rows x 4 column tiles): the 128 x 64 tile re-reads its A rows once per 64
     // output columns and its weights once per 128 rows, and at these sizes that L2 -> CU
     // stream, not the MFMA, was the bound.  Only when they still leave wide_min workgroups.
-    static const int64_t wide_min = getenv("PN2_DENSE_WIDE_MINWG") ? atol(getenv("PN2_DENSE_WIDE_MINWG")) : 512;
+    const int64_t wide_min = getenv("PN2_DENSE_WIDE_MINWG") ? atol(getenv("PN2_DENSE_WIDE_MINWG")) : 512;
     const bool wide = A.tiles % 4 == 0 && (A.M + 255) / 256 * (A.tiles / 4) >= wide_min;
     const int64_t kRowsSel = wide ? 256 : kDRows;
     // otherwise the widest tile (NTC 32-column tiles per wave) that still leaves min_wg workgroups

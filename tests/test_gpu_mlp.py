@@ -203,7 +203,7 @@ GROUP_ALL = [
 ]
 
 
-@pytest.mark.parametrize("path", ["split", "f32"])
+@pytest.mark.parametrize("path", ["split", "f32", "wide"])
 @pytest.mark.parametrize("case", range(len(GROUP_ALL)))
 def test_group_all_vs_oracle(case, path, monkeypatch):
     import pn2
@@ -213,6 +213,9 @@ def test_group_all_vs_oracle(case, path, monkeypatch):
         monkeypatch.setenv("PN2_MLP_PATH", "f32")
     else:
         monkeypatch.delenv("PN2_MLP_PATH", raising=False)
+    if path == "wide":  # the 256 x 128 (8-wave) dense tiles of large layers, at a small size
+        monkeypatch.setenv("PN2_DENSE_WIDE_MINWG", "1")
+        path = "split"
     B = 3
     pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 400 + case)
     feat = torch.randn(B, N, D, generator=torch.Generator().manual_seed(500 + case)) if D else None
