@@ -72,6 +72,10 @@ struct DenseSplitArgs {
     int64_t ostride;
     int raw;        // 1: out = A . W^T as accumulated (no BN / ReLU; the chain's layer-0 pre-pass)
     int norelu;     // 1: out = alpha * (A . W^T) + beta, no ReLU (signed values: pooled as keys)
+    // side job: zero [zrows][zcols] floats at `zero` (row stride zstride) -- the NEXT layer's
+    // atomicMax pool, so that layer needs no memset launch of its own
+    float *zero;
+    int64_t zrows, zcols, zstride;
 };
 
 // Signed max through unsigned atomics: key() is monotone from float order to uint order (and
@@ -121,6 +125,15 @@ void dense_split_kernel(const DenseSplitArgs A) {
     const int gpb = A.pool_mode == 1 ? kDRows / A.K : 0;
     if (A.pool_mode == 1)
         for (int e = tid; e < gpb * ncols; e += 64 * kDW) opool[e] = 0.f;
+    if (A.zero) {  // this workgroup's share of the next layer's pool (stream order publishes it)
+        const int64_t tot = A.zrows * A.zcols, nwg = (int64_t)gridDim.x * gridDim.y;
+        const int64_t per = (tot + nwg - 1) / nwg, e0 = (int64_t)(blockIdx.x + blockIdx.y * gridDim.x) * per;
+        const int64_t e1 = e0 + per < tot ? e0 + per : tot;
+        for (int64_t e = e0 + tid; e < e1; e += 64 * kDW) {
+            const int64_t g = e / A.zcols;
+            A.zero[g * A.zstride + (e - g * A.zcols)] = 0.f;
+        }
+    }
 
     // ---- this lane's row (A operand)
     const int R = row0 + 32 * wave + r;
@@ -407,14 +420,25 @@ static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
     return PN2_OK;
 }
 
-static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
+// Large layers take 256 x 128 tiles (see dense_split_layer); the rows a launch's workgroup
+// covers decide which pools fit in LDS
+static bool dense_wide(const DenseSplitArgs &A) {
+    const int64_t wide_min = getenv("PN2_DENSE_WIDE_MINWG") ? atol(getenv("PN2_DENSE_WIDE_MINWG")) : 512;
+    return A.tiles % 4 == 0 && (A.M + 255) / 256 * (A.tiles / 4) >= wide_min;
+}
+static int dense_pool_mode(const DenseSplitArgs &A) {
+    const int64_t kRowsSel = dense_wide(A) ? 256 : kDRows;
+    if (A.K == 8 || A.K == 16) return 0;
+    if (A.K % 32 == 0 && kRowsSel % A.K == 0) return 1;
+    return 2;
+}
+
+static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st, bool prezeroed = false) {
     // Large layers (e.g. translation_ssg's group_all over B*512 rows) take 256 x 128 tiles (8
     // waves of 32 rows x 4 column tiles): the 128 x 64 tile re-reads its A rows once per 64
     // output columns and its weights once per 128 rows, and at these sizes that L2 -> CU
     // stream, not the MFMA, was the bound.  Only when they still leave wide_min workgroups.
-    const int64_t wide_min = getenv("PN2_DENSE_WIDE_MINWG") ? atol(getenv("PN2_DENSE_WIDE_MINWG")) : 512;
-    const bool wide = A.tiles % 4 == 0 && (A.M + 255) / 256 * (A.tiles / 4) >= wide_min;
-    const int64_t kRowsSel = wide ? 256 : kDRows;
+    const bool wide = dense_wide(A);
     // otherwise the widest tile (NTC 32-column tiles per wave) that still leaves min_wg workgroups
     const int64_t rowblocks = (A.M + kDRows - 1) / kDRows;
     static const int64_t min_wg = getenv("PN2_DENSE_MINWG") ? atol(getenv("PN2_DENSE_MINWG")) : 512;
@@ -426,10 +450,8 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st) {
             break;
         }
     if (A.pool) {
-        if (A.K == 8 || A.K == 16) A.pool_mode = 0;
-        else if (A.K % 32 == 0 && kRowsSel % A.K == 0) A.pool_mode = 1;
-        else A.pool_mode = 2;
-        if (A.pool_mode == 2) {
+        A.pool_mode = dense_pool_mode(A);
+        if (A.pool_mode == 2 && !prezeroed) {
             const int64_t G = A.M / A.K, cols = 32 * (int64_t)A.tiles;
             hipError_t e = A.ostride == cols
                                ? hipMemsetAsync(A.out, 0, (size_t)G * cols * 4, st)
@@ -495,8 +517,7 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
     const int64_t w = dense_split_width(s, layers, nlayers, np);
     if (w == 0) return 0;
     if (nlayers > 1 && (!ws || ws_bytes < 2 * M * w * 4 || ((uintptr_t)ws & 15))) return 0;
-    const bool vec_rows_ok = true;
-    for (int l = 0; l < nlayers; ++l) {
+    auto make = [&](int l) {
         const bool last = l == nlayers - 1;
         DenseSplitArgs A;
         memset(&A, 0, sizeof(A));
@@ -518,7 +539,7 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
                 A.rs = w;
             }
             A.cin = (int)layers[l].cin;
-            A.vec = (vec_rows_ok && ((uintptr_t)A.rows & 15) == 0 && A.rs % 4 == 0) ? 1 : 0;
+            A.vec = (((uintptr_t)A.rows & 15) == 0 && A.rs % 4 == 0) ? 1 : 0;
             A.kb = (int)((layers[l].cin + 15) / 16);
         }
         A.w = reinterpret_cast<const bf16x8 *>(layers[l].wt_split);
@@ -531,7 +552,21 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
         A.K = (int)K;
         A.out = last ? out : ws + (l & 1) * M * w;
         A.ostride = last ? ostride : w;
-        const int rc = dense_split_layer(A, np, st);
+        return A;
+    };
+    // a last layer that pools by HBM atomics gets its output zeroed by the layer before it
+    // (one launch fewer than a memset: PointNet-v1's max over N points, group_all over K > 256)
+    DenseSplitArgs last = make(nlayers - 1);
+    const bool fold_zero = nlayers > 1 && last.pool && dense_pool_mode(last) == 2;
+    for (int l = 0; l < nlayers; ++l) {
+        DenseSplitArgs A = l == nlayers - 1 ? last : make(l);
+        if (fold_zero && l == nlayers - 2) {
+            A.zero = last.out;
+            A.zrows = last.M / last.K;
+            A.zcols = 32 * (int64_t)last.tiles;
+            A.zstride = last.ostride;
+        }
+        const int rc = dense_split_layer(A, np, st, fold_zero && l == nlayers - 1);
         if (rc != PN2_OK) return rc;
     }
     return 1;
