@@ -576,8 +576,17 @@ class GraphedPipeline(PipelinedForward):
             return []
         extra_of = (lambda i: ()) if extras is None else (lambda i: tuple(extras[i]))
         key = self._state_key(batches[0], extra_of(0))
-        if any(self._state_key(x, extra_of(i))[0] != key[0] for i, x in enumerate(batches)):
-            return self._run_eager(batches, extras, post, False)  # mixed shapes: eager
+        # the other batches need only the same input signature (the full key walks every
+        # parameter and buffer: ~30 us of host time per batch before the first launch, all of it
+        # GPU idle time inside a timed run); a batch list repeating one input needs nothing
+        from .graphs import _sig
+        x0, e0 = batches[0], extra_of(0)
+        for i in range(1, len(batches)):
+            x = batches[i]
+            if x is x0 and (extras is None or all(a is b for a, b in zip(extra_of(i), e0))):
+                continue
+            if _sig((x,) + extra_of(i)) != key[0]:
+                return self._run_eager(batches, extras, post, False)  # mixed shapes: eager
         outs, first = [], 0
         dev = batches[0].device
         if key != self._key or self._slots is None:
@@ -646,17 +655,29 @@ class GraphedPipeline(PipelinedForward):
                 ev_fps[s] = geo.record_event()
                 mark(js[0] - first, "geo1", geo)
 
+        issued = [0]  # geometry groups issued so far (always in group order: the draw order)
+
+        def top_up(force, limit):
+            # every group <= force now (a batch's own group), then at most one more while it
+            # stays <= limit: group j takes the slot of group j - ng, so it waits until that
+            # group's batches are all issued (their ev_read events exist).  One group per batch
+            # interleaves the host's geometry issue with the compute issue, so the first batch's
+            # sa graph is issued right behind its geometry, not behind ng-1 groups of it
+            while issued[0] <= min(force, ngr - 1):
+                issue_fps(issued[0])
+                issued[0] += 1
+            if issued[0] <= min(limit, ngr - 1):
+                issue_fps(issued[0])
+                issued[0] += 1
+
         with torch.no_grad():
-            # the geometry runs ng-1 groups ahead of the compute stream
-            for g in range(min(ng - 1, ngr)):
-                issue_fps(g)
+            # the geometry runs up to ng-1 groups ahead of the compute streams
             for i in range(first, len(batches)):
                 g, h = divmod(i - first, gb)
                 s = g % ng
                 bs = s * gb + h
                 sl = self._slots[s].halves[h]
-                if h == 0 and g + ng - 1 < ngr:
-                    issue_fps(g + ng - 1)
+                top_up(g, -1)
                 main = mains[(i - first) % len(mains)]
                 with torch.cuda.stream(main):
                     main.wait_event(ev_fps[s])
@@ -695,6 +716,7 @@ class GraphedPipeline(PipelinedForward):
                                 t.record_stream(tail)
                         out = post(i, out)
                 outs.append(out)
+                top_up(-1, (g if h == gb - 1 else g - 1) + ng)
         for g in geos[1:]:
             geo.wait_stream(g)
         self._pinned_evs[self._pinned_cur] = geo.record_event()  # uploads read it
