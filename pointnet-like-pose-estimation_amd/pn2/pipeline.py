@@ -441,7 +441,8 @@ class GraphedPipeline(PipelinedForward):
             raise ValueError("pn2.pipeline: compute_streams=2 needs shared CUs (geometry_cus=0)")
         self.compute_streams = int(compute_streams)
         # the head graphs get the tail stream while the queues allow it
-        self.head_on_tail = geometry_streams + self.compute_streams + 1 <= 4
+        self.head_on_tail = (geometry_streams + self.compute_streams + 1 <= 4 and
+                             os.environ.get("PN2_HEADS_ON_COMPUTE", "") != "1")  # A/B knob
         self.nslots = int(nslots)
         self.gb = gb
         self.ngroups = self.nslots // gb
