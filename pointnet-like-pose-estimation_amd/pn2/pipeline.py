@@ -605,6 +605,18 @@ class GraphedPipeline(PipelinedForward):
             self._slots = [self._capture(batches[0], extra_of(0), dev, draws)
                            for _ in range(self.ngroups)]
             self._key = self._state_key(batches[0], extra_of(0))
+            # replay every captured graph once now, in dependency order on this stream (start
+            # index 0: a valid point; outputs land in static buffers that real replays
+            # overwrite; no RNG inside the graphs): a graph's first launch costs extra, and
+            # otherwise the slots a short first run does not reach pay it in the next one
+            for grp in self._slots:
+                grp.start_buf.zero_()
+                grp.fps.replay()
+                for sl in grp.halves:
+                    sl.sa.replay()
+                    if sl.head is not None:
+                        sl.head.replay()
+            torch.cuda.synchronize(dev)
             first = 1
         if first == len(batches):
             return outs
