@@ -27,6 +27,24 @@ def _sig(args):
     return tuple((tuple(a.shape), tuple(a.stride()), a.dtype, a.device) for a in args)
 
 
+def _module_tensors(model):
+    """Every parameter and buffer of `model` (the same tensors as parameters() + buffers(),
+    shared ones possibly twice): a direct walk of the module tree, ~6x cheaper on the host than
+    the generator chain, which took 160-240 us for a PointNet++ head -- paid per replay call
+    by the graph key below."""
+    out = []
+
+    def walk(m):
+        out.extend(t for t in m._parameters.values() if t is not None)
+        out.extend(t for t in m._buffers.values() if t is not None)
+        for c in m._modules.values():
+            if c is not None:
+                walk(c)
+
+    walk(model)
+    return out
+
+
 class GraphedForward:
     def __init__(self, model):
         self.model = model
@@ -34,7 +52,7 @@ class GraphedForward:
         self._graph = None
 
     def _state_key(self, args):
-        ts = list(self.model.parameters()) + list(self.model.buffers())
+        ts = _module_tensors(self.model)
         return (_sig(args), ops.current_precision()) + tuple((t.data_ptr(), t._version) for t in ts)
 
     def _eager(self, args):

@@ -452,8 +452,8 @@ class GraphedPipeline(PipelinedForward):
         self._slots = None  # the group slots
 
     def _state_key(self, x, extra):
-        from .graphs import _sig
-        ts = list(self.model.parameters()) + list(self.model.buffers())
+        from .graphs import _module_tensors, _sig
+        ts = _module_tensors(self.model)
         return (_sig((x,) + tuple(extra)), ops.current_precision()) + tuple(
             (t.data_ptr(), t._version) for t in ts)
 
