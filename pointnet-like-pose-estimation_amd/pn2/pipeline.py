@@ -122,7 +122,9 @@ def _streams(device, geometry_cus):
         lo, hi = torch.cuda.Stream.priority_range()
         geo = torch.cuda.Stream(dev, priority=min(lo, hi))
         geo2 = torch.cuda.Stream(dev, priority=min(lo, hi))
-        main, tail = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        main = torch.cuda.Stream(dev)
+        # PN2_TAIL_PRIO=1: the tail (heads) at high priority as well (A/B knob)
+        tail = torch.cuda.Stream(dev, priority=min(lo, hi) if os.environ.get("PN2_TAIL_PRIO") == "1" else 0)
         main2 = torch.cuda.default_stream(dev)
         for st in (geo, main, tail):
             with torch.cuda.stream(st):
