@@ -670,6 +670,7 @@ class GraphedPipeline(PipelinedForward):
                 ev_fps[s] = geo.record_event()
                 mark(js[0] - first, "geo1", geo)
 
+        drain = int(os.environ.get("PN2_DRAIN_HEADS", "2"))  # see the head stream choice below
         issued = [0]  # geometry groups issued so far (always in group order: the draw order)
 
         def top_up(force, limit):
@@ -704,7 +705,11 @@ class GraphedPipeline(PipelinedForward):
                     sl.sa.replay()
                     ev_sa = main.record_event()
                     mark(i - first, "sa1", main)
-                ts = tail if sl.head is not None and self.head_on_tail else main
+                # the last `drain` batches run their heads on their own (by then idle)
+                # compute streams: the tail stream runs ~2 heads behind the sa graphs, and at
+                # the end of a run that backlog is the drain
+                ts = tail if (sl.head is not None and self.head_on_tail and
+                              i < len(batches) - drain) else main
                 with torch.cuda.stream(ts):
                     if sl.head is not None:
                         if ts is not main:
