@@ -175,7 +175,7 @@ def step(names, models, x, mean, gB, lo):
         for n, m in zip(names, models):
             o = m(x, mean) if n.startswith("translation") else m(x)
             o = o[0] if isinstance(o, tuple) else o
-            outs.append(shard.all_gather_rows(o))
+            outs.append(shard.all_gather_rows(o, sizes="shard"))
     return outs
 
 
@@ -225,6 +225,30 @@ def load_traffic(cfg, op="pn2_sa_mlp_max_f32"):
         return d.get(cfg, {}).get(op)
     except (OSError, ValueError):
         return None
+
+
+def count_gpus(topology="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this process may use, counted without initialising HIP: the KFD topology's GPU
+    nodes (simd_count > 0), capped by HIP_/ROCR_/CUDA_VISIBLE_DEVICES.  The launcher's parent
+    forks its ranks afterwards, so it must not have touched the GPU runtime (torch's
+    device_count() falls back to initialising HIP when amdsmi does not answer)."""
+    n = 0
+    try:
+        for node in os.listdir(topology):
+            try:
+                with open(os.path.join(topology, node, "properties")) as fh:
+                    props = dict(line.split(None, 1) for line in fh if line.strip())
+            except (OSError, ValueError):
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        return 0
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip()]))
+    return n
 
 
 def rank_envs(n, port, base=None):
@@ -284,9 +308,10 @@ def main():
     a = parse()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and a.gpus > 1:
-        ndev = torch.cuda.device_count()  # counts devices without initialising one
-        if ndev < a.gpus and not a.plumbing_check:
-            sys.exit("bench.py: --gpus %d but only %d device(s) visible" % (a.gpus, ndev))
+        if not a.plumbing_check:
+            ndev = count_gpus()  # no HIP call in the parent: it forks the ranks next
+            if ndev < a.gpus:
+                sys.exit("bench.py: --gpus %d but only %d device(s) visible" % (a.gpus, ndev))
         sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
     if env_world is not None and int(env_world) != a.gpus:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s (the launcher started %s ranks)"
@@ -346,8 +371,9 @@ def main():
 
     def gather(i, o):  # step()'s all_gather of every head's first output
         if len(names) > 1:
-            return [shard.all_gather_rows(h[0] if isinstance(h, tuple) else h) for h in o]
-        return shard.all_gather_rows(o[0] if isinstance(o, tuple) else o)
+            return [shard.all_gather_rows(h[0] if isinstance(h, tuple) else h, sizes="shard")
+                    for h in o]
+        return shard.all_gather_rows(o[0] if isinstance(o, tuple) else o, sizes="shard")
 
     def run_pipelined(k):
         with shard.batch_shard(gB, lo):

@@ -8,9 +8,11 @@
  *   - is asynchronous on that stream and never synchronises the device, so it may be captured
  *     into a hipGraph;
  *   - returns PN2_OK (0) or a negative PN2_E* code; the message of the last failure on the
- *     calling thread is returned by pn2_last_error() (thread-local: the library holds no other
- *     mutable global state, so it is re-entrant across host threads, as the reference's
- *     concurrent-inference demo /root/reference/mutilthreading/predict_test.py:44-63 requires).
+ *     calling thread is returned by pn2_last_error() (thread-local).  Besides it the library
+ *     holds only the tuning parameters (set by tests / A/B tools) and the sticky device error
+ *     word below, which kernels only ever OR into -- so calls are re-entrant across host
+ *     threads, as the reference's concurrent-inference demo
+ *     /root/reference/mutilthreading/predict_test.py:44-63 requires.
  *
  * Reference interfaces replaced (file:line in /root/reference):
  *   pn2_fps_f32            farthest_point_sample            model/pointnet2_utils.py:47-68
@@ -55,10 +57,32 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 9
+#define PN2_ABI_VERSION 10
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
+
+/* Device error word: conditions under which the reference raises but a kernel cannot.  The
+ * kernels stay in bounds (clamped or NaN outputs, documented per entry point) and OR a bit into
+ * a per-device word; pn2_device_errors reads it (synchronously: it waits for the device's
+ * work) and clears it when `clear` != 0.  pn2.check_device_errors() raises IndexError.
+ *   PN2_DEVERR_NO_NEIGHBOUR  a ball-query centroid had no point within the radius (its row is
+ *                            padded with N, pointnet2_utils.py:85-89; the reference's next
+ *                            index_points raises IndexError); the SA kernels read point 0 there
+ *   PN2_DEVERR_INDEX         pn2_index_points_f32 / pn2_group_f32 got an index outside [-N, N)
+ *                            (the element is NaN) */
+#define PN2_DEVERR_NO_NEIGHBOUR 1u
+#define PN2_DEVERR_INDEX 2u
+int pn2_device_errors(int clear, uint32_t *bits);
+
+/* Kernel-selection tuning: process-wide int64 parameters of the launch choices (which kernel
+ * family, tile widths, block shapes).  The defaults are the measured best and the library never
+ * reads the environment; tests and A/B tools change them (pn2/tuning.py applies the one
+ * PN2_TUNING="key=value,..." variable at load).  Change them only while no pn2 call is in
+ * flight on another host thread.  Keys: pn2_tuning_keys() (space-separated). */
+int pn2_tuning_get(const char *key, int64_t *value);
+int pn2_tuning_set(const char *key, int64_t value);
+const char *pn2_tuning_keys(void);
 
 /* Packed point layout used by the ball query: [B][N][cp] float32, cp = pn2_packed_stride(C),
  * holding the C coordinates, then ssq = torch.sum(p**2,-1) computed with the reference's
@@ -163,8 +187,8 @@ typedef struct pn2_mlp_layer {
  * (0 for padding).  kblocks = pn2_layer_split_kblocks(cin, xyz); the image takes
  * pn2_layer_split_bytes(cout, cin, xyz) bytes, 16-byte aligned.  Chains given wt_split for
  * every layer (3 layers, grouped rows, hidden widths 32..128) run as one register-resident
- * kernel with fp32-accurate 6-product bf16 MFMA arithmetic; others (and PN2_MLP_PATH=f32) use
- * the fp32 MFMA kernels. */
+ * kernel with fp32-accurate 6-product bf16 MFMA arithmetic; others (and tuning mlp_f32 = 1)
+ * use the fp32 MFMA kernels. */
 int64_t pn2_layer_split_kblocks(int64_t cin, int64_t xyz);
 int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin, int64_t xyz);
 int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t xyz,

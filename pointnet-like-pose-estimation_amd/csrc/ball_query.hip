@@ -38,6 +38,22 @@
 
 namespace pn2 {
 
+// raised when a valid centroid has no point within the radius: its row is padded with index N
+// (the reference's out-of-range pad, pointnet2_utils.py:85-89, which makes its index_points
+// raise IndexError); the SA kernels clamp such indices instead of reading past the cloud
+__device__ unsigned g_bq_errors;
+
+int read_bq_errors(unsigned *bits, int clear) {
+    unsigned v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_bq_errors), sizeof(v)) != hipSuccess) return -1;
+    if (clear && v) {
+        const unsigned z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bq_errors), &z, sizeof(z)) != hipSuccess) return -1;
+    }
+    *bits = v;
+    return 0;
+}
+
 // CC > 0: the channel count is known at compile time (C = 3 xyz, C = 10 pose) and the shape is
 // not ATen's naive-bmm size; CC = 0: runtime C and the `small` flag.  NW bitmask words per
 // segment (TS = 32*NW points per wave per round).
@@ -177,6 +193,7 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
         if (g0 + j >= S) break;
         const int cj = min(__builtin_amdgcn_readlane(total, j), K);
         const int fj = firsts[j];
+        if (cj == 0 && lane == 0) atomicOr(&g_bq_errors, (unsigned)PN2_DEVERR_NO_NEIGHBOUR);
         int64_t *o = out + ((int64_t)b * S + g0 + j) * K;
         for (int k = cj + lane; k < K; k += 64) o[k] = fj;
         if (out_cnt && lane == 0) out_cnt[(int64_t)b * S + g0 + j] = cj;
@@ -193,9 +210,9 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
     const int64_t nblk = B * ((S + 63) / 64);
     PN2_REQUIRE(nblk < (int64_t)1 << 31, "pn2_ball_query_f32: too many centroids");
     // waves per workgroup: 16 for long xyz clouds (more segments in flight), else 8
-    // (profiles/r02_bq/bq_modes.txt); PN2_BQ_WAVES=8|16 overrides (tuning)
+    // (profiles/r02_bq/bq_modes.txt); tuning bq_waves = 8 | 16 overrides
     int P = (CP == 4 && N >= 2048) ? 16 : 8;
-    if (const char *e = getenv("PN2_BQ_WAVES")) P = atoi(e) == 16 ? 16 : 8;
+    if (tuning().bq_waves) P = tuning().bq_waves == 16 ? 16 : 8;
     // words per segment: a round stages up to P*32*nw records (<= 64 per wave beyond xyz)
     const int64_t per_wave = (N + P - 1) / P;
     int nw = per_wave <= 32 ? 1 : per_wave <= 64 ? 2 : 4;

@@ -370,15 +370,14 @@ static int launch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t
     return PN2_OK;
 }
 
-// Block shape per cloud size.  PN2_FPS_CFG="<threads>x<points per thread>" forces one of the
-// compiled shapes (tuning experiments only).
+// Block shape per cloud size.  Tuning fps_threads / fps_ppt force one of the compiled shapes
+// (tuning experiments only).
 template <int CM, bool FIXED, int CAP>
 static int dispatch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
                         int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx,
                         float *out_pts, float *out_packed, float *pts_packed, hipStream_t st) {
 #define A pts, B, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed, st
-    int fnt = 0, fppt = 0;
-    if (const char *e = getenv("PN2_FPS_CFG")) sscanf(e, "%dx%d", &fnt, &fppt);
+    const int64_t fnt = tuning().fps_threads, fppt = tuning().fps_ppt;
 #define PN2_FPS_TRY(nt, ppt) \
     if (fnt == nt && fppt == ppt && N <= (int64_t)nt * ppt) return launch_fps<nt, ppt, CM, FIXED>(A);
     PN2_FPS_TRY(64, 8) PN2_FPS_TRY(64, 16) PN2_FPS_TRY(128, 4) PN2_FPS_TRY(128, 8) PN2_FPS_TRY(256, 2)

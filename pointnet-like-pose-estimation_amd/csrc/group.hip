@@ -7,9 +7,37 @@
 // tensors; these kernels serve the standalone functions of the drop-in module.
 // One thread per output element (contiguous output => coalesced stores); the subtraction is a
 // single correctly rounded float32 op, bit-identical to the reference.
+//
+// Indices follow torch's advanced indexing: -N <= n < 0 counts from the end.  Outside [-N, N)
+// the reference raises IndexError; a kernel cannot, so the element is NaN (never an
+// out-of-bounds read) and PN2_DEVERR_INDEX is raised in the device error word
+// (pn2_device_errors; pn2.check_device_errors() raises IndexError).
 #include "pn2_internal.h"
 
 namespace pn2 {
+
+__device__ unsigned g_group_errors;
+
+// torch's index rule; -1 when out of range (and the error word raised)
+__device__ __forceinline__ int64_t torch_index(int64_t n, int64_t N) {
+    if (n < 0) n += N;
+    if (n < 0 || n >= N) {
+        atomicOr(&g_group_errors, (unsigned)PN2_DEVERR_INDEX);
+        return -1;
+    }
+    return n;
+}
+
+int read_group_errors(unsigned *bits, int clear) {
+    unsigned v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_group_errors), sizeof(v)) != hipSuccess) return -1;
+    if (clear && v) {
+        const unsigned z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_group_errors), &z, sizeof(z)) != hipSuccess) return -1;
+    }
+    *bits = v;
+    return 0;
+}
 
 __global__ __launch_bounds__(256) void index_points_kernel(const float *__restrict__ pts,
                                                            int64_t B, int64_t N, int64_t C,
@@ -21,8 +49,8 @@ __global__ __launch_bounds__(256) void index_points_kernel(const float *__restri
     const int64_t c = e % C;
     const int64_t bm = e / C;
     const int64_t b = bm / M;
-    const int64_t n = idx[bm];
-    out[e] = pts[b * sb + n * sn + c * sc];
+    const int64_t n = torch_index(idx[bm], N);
+    out[e] = n < 0 ? __builtin_nanf("") : pts[b * sb + n * sn + c * sc];
 }
 
 __global__ __launch_bounds__(256) void group_kernel(const float *__restrict__ pts, int64_t N,
@@ -40,10 +68,12 @@ __global__ __launch_bounds__(256) void group_kernel(const float *__restrict__ pt
     const int64_t row = e / W;  // (b*S + s)*K + k
     const int64_t g = row / K;
     const int64_t b = g / S;
-    const int64_t n = idx[row];
+    const int64_t n = torch_index(idx[row], N);
     const int64_t xc = feature_first ? ch - D : ch;  // xyz channel, if any
     float v;
-    if (xc >= 0 && xc < C)
+    if (n < 0)
+        v = __builtin_nanf("");
+    else if (xc >= 0 && xc < C)
         v = __fsub_rn(pts[b * sb + n * sn + xc * sc], ctr[g * C + xc]);
     else {
         const int64_t d = feature_first ? ch : ch - C;

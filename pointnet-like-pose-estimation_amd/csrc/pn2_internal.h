@@ -26,6 +26,35 @@ int set_error(int code, const char *fmt, ...);
 
 static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ------------------------------------------------------------------ kernel-selection tuning
+// Process-wide parameters of the launch choices (defaults = the measured best).  Nothing reads
+// the environment: tests and A/B tools set them through pn2_tuning_set (pn2/tuning.py parses
+// the one PN2_TUNING variable).  X(name, default)
+#define PN2_TUNING_KEYS(X)                                                                     \
+    X(mlp_f32, 0)          /* 1: fp32 MFMA kernels instead of the split-bf16 ones          */ \
+    X(chain_prepass, 1)    /* 0: no layer-0 pre-pass (wide first layers of a chain)        */ \
+    X(compact, 1)          /* 0: no compact neighbourhoods (every padded row computed)     */ \
+    X(compact_pool, 0)     /* LDS pool rows of compact chain launches (0: automatic)       */ \
+    X(compact_stages, 2)   /* weight-ring stages of compact chain launches (2 or 3)        */ \
+    X(bq_waves, 0)         /* ball query waves per workgroup (0: automatic, 8 or 16)       */ \
+    X(fps_threads, 0)      /* FPS block shape threads x points per thread (0: automatic)   */ \
+    X(fps_ppt, 0)                                                                              \
+    X(dense_maxntc, 2)     /* widest 32-column tile count of the 4-wave dense layer         */ \
+    X(dense_minwg, 512)    /* workgroups a wider dense tile must still leave                 */ \
+    X(dense_wide_minwg, 512) /* workgroups the 256 x 128 dense tile must leave              */
+
+struct Tuning {
+#define PN2_TUNING_FIELD(name, dflt) int64_t name = dflt;
+    PN2_TUNING_KEYS(PN2_TUNING_FIELD)
+#undef PN2_TUNING_FIELD
+};
+const Tuning &tuning();
+
+// device error words (pn2_device_errors): each translation unit that can raise one keeps its
+// own __device__ word; these read (and optionally clear) it, synchronously
+int read_group_errors(unsigned *bits, int clear);
+int read_bq_errors(unsigned *bits, int clear);
+
 constexpr int kMaxC = 16;  // point dims (xyz + one-hot) held in registers
 
 // np: bf16 planes per operand -- 3 = fp32-accurate split products, 1 = plain bf16 products

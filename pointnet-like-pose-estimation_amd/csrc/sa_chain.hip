@@ -300,6 +300,9 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         g = valid ? R / (unsigned)A.K : 0u;
         n = valid ? (int)s.idx[R] : 0;
     }
+    // a centroid with no neighbour in its radius is padded with N (the ball query raises
+    // PN2_DEVERR_NO_NEIGHBOUR): read point 0 there, never past the cloud
+    if ((unsigned)n >= (unsigned)s.N) n = 0;
     const unsigned b = g / (unsigned)A.S;
     const float *frow = s.feat ? s.feat + (int64_t)b * s.fb + (int64_t)n * s.fn : nullptr;
     const float *prow = s.pts + (int64_t)b * s.pb + (int64_t)n * s.pn;
@@ -886,8 +889,7 @@ static int chain_kb0m(int T0, int T1, int kb0) {
 static bool chain_use_prepass(const pn2_sa_src &s, const pn2_mlp_layer *layers, int T0, int T1,
                               int kb0, int64_t M, int np) {
     if (np != 3 || kb0 < 5 || s.C < 1 || s.C > kMaxC || !layers[0].wt) return false;
-    if (const char *e = getenv("PN2_CHAIN_PREPASS"))
-        if (strcmp(e, "0") == 0) return false;
+    if (!tuning().chain_prepass) return false;
     if (4 * s.B * s.N > M) return false;
     bool has = false;
 #define PN2_CHAIN_HAS(a, b, c) \
@@ -915,8 +917,8 @@ static bool chain_shape(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nl
 }
 
 // compact neighbourhoods (pool_mode 3): groups of K in [9, 128] (K <= 8 is one unit anyway),
-// given the ball query's counts, the scan kernel's LDS within one CU's 160 KB.  PN2_COMPACT=0
-// disables (A/B); PN2_COMPACT_KS=3 keeps the 3-stage ring.
+// given the ball query's counts, the scan kernel's LDS within one CU's 160 KB.  Tuning
+// compact = 0 disables (A/B); compact_stages = 3 keeps the 3-stage ring.
 static int64_t compact_wpc(const pn2_sa_src &s) {
     return (s.S * ((s.K + kUnitRows - 1) / kUnitRows) + kUnitsPerWG - 1) / kUnitsPerWG;
 }
@@ -926,8 +928,7 @@ static size_t compact_scan_lds(const pn2_sa_src &s) {
 static bool chain_use_compact(const pn2_sa_src &s) {
     if (!s.cnt || s.K <= kUnitRows || s.K > 128 || s.S < 1) return false;
     if (compact_scan_lds(s) > (size_t)160 * 1024) return false;
-    if (const char *e = getenv("PN2_COMPACT"))
-        if (strcmp(e, "0") == 0) return false;
+    if (!tuning().compact) return false;
     return true;
 }
 static int64_t compact_table_bytes(const pn2_sa_src &s) {
@@ -959,8 +960,7 @@ int64_t chain_prepass_bytes(const pn2_sa_src &s, const pn2_mlp_layer *layers, in
 int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
                      float *out, int64_t ostride, int64_t M, int64_t K, int np, float *ws,
                      int64_t ws_bytes, hipStream_t st) {
-    if (const char *e = getenv("PN2_MLP_PATH"))
-        if (np == 3 && strcmp(e, "f32") == 0) return 0;
+    if (np == 3 && tuning().mlp_f32) return 0;
     // k-blocks per layer (the first layer's rows are [xyz | features], see split_in_channel)
     int T0, T1, kbs[3];
     if (!chain_shape(s, layers, nlayers, pool, T0, T1, kbs)) return 0;
@@ -997,7 +997,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     // 130 us, although each workgroup lived 36 us instead of 45: tools/debug/chain_stamps.py).
     // An 8-row pool (groups past it merge through HBM atomics into rows the scan zeroed) keeps
     // 3 per CU with 3 stages -- measured 117.8 vs 114.2 us, so the default stays 2 stages;
-    // PN2_COMPACT_KS=3 selects the 3-stage ring with the 8-row pool when it keeps the
+    // tuning compact_stages = 3 selects the 3-stage ring with the 8-row pool when it keeps the
     // workgroups per CU the registers allow (A/B, and the tests of the overflow path).
     int cks = 2, cprow = kUnitsPerWG;
     if (compact) {
@@ -1011,9 +1011,9 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         // an 8-row pool when it buys a workgroup per CU (SSG sa1: 4 -> 5 per CU, 62.4 -> 59.9
         // us; its many small groups past the 8th of a workgroup merge through HBM atomics)
         if (wgs(2, 8) > wgs(2, kUnitsPerWG)) cprow = 8;
-        if (const char *e = getenv("PN2_COMPACT_POOL"))  // A/B override of the pool rows
-            cprow = std::max(1, std::min<int>(kUnitsPerWG, atoi(e)));
-        if (getenv("PN2_COMPACT_KS") && getenv("PN2_COMPACT_KS")[0] == '3' && wgs(3, 8) >= wgs(2, kUnitsPerWG))
+        if (tuning().compact_pool > 0)  // A/B override of the pool rows
+            cprow = (int)std::max<int64_t>(1, std::min<int64_t>(kUnitsPerWG, tuning().compact_pool));
+        if (tuning().compact_stages == 3 && wgs(3, 8) >= wgs(2, kUnitsPerWG))
             cks = 3, cprow = 8;
     }
     int *cunits = nullptr;

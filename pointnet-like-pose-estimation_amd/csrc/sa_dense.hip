@@ -423,7 +423,7 @@ static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
 // Large layers take 256 x 128 tiles (see dense_split_layer); the rows a launch's workgroup
 // covers decide which pools fit in LDS
 static bool dense_wide(const DenseSplitArgs &A) {
-    const int64_t wide_min = getenv("PN2_DENSE_WIDE_MINWG") ? atol(getenv("PN2_DENSE_WIDE_MINWG")) : 512;
+    const int64_t wide_min = tuning().dense_wide_minwg;
     return A.tiles % 4 == 0 && (A.M + 255) / 256 * (A.tiles / 4) >= wide_min;
 }
 static int dense_pool_mode(const DenseSplitArgs &A) {
@@ -441,8 +441,8 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st, bool pre
     const bool wide = dense_wide(A);
     // otherwise the widest tile (NTC 32-column tiles per wave) that still leaves min_wg workgroups
     const int64_t rowblocks = (A.M + kDRows - 1) / kDRows;
-    static const int64_t min_wg = getenv("PN2_DENSE_MINWG") ? atol(getenv("PN2_DENSE_MINWG")) : 512;
-    static const int max_ntc = getenv("PN2_DENSE_MAXNTC") ? atoi(getenv("PN2_DENSE_MAXNTC")) : 2;
+    const int64_t min_wg = tuning().dense_minwg;
+    const int max_ntc = (int)tuning().dense_maxntc;
     int ntc = 1;
     for (int t = max_ntc; t > 1; t /= 2)
         if (A.tiles % t == 0 && rowblocks * (A.tiles / t) >= min_wg) {
@@ -498,7 +498,7 @@ int launch_layer0_prepass(const pn2_sa_src &s, const pn2_mlp_layer &L0, float *z
 
 // Widest hidden layer of a chain the split dense path runs layer by layer (0: not eligible).
 int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np) {
-    if (np == 3 && getenv("PN2_MLP_PATH") && strcmp(getenv("PN2_MLP_PATH"), "f32") == 0) return 0;
+    if (np == 3 && tuning().mlp_f32) return 0;
     if (s.mode != PN2_SRC_GROUP_ALL && s.mode != PN2_SRC_ROWS) return 0;
     if (s.mode == PN2_SRC_GROUP_ALL && s.C > 16) return 0;
     int64_t w = 0;

@@ -85,6 +85,7 @@ __device__ __forceinline__ void gather_rows(const MlpArgs &A, float *act, int *r
                 const unsigned g = R / (unsigned)s.K;
                 b = (int)(g / (unsigned)s.S);
                 n = (int)s.idx[R];
+                if ((unsigned)n >= (unsigned)s.N) n = 0;  // no-neighbour pad (PN2_DEVERR_NO_NEIGHBOUR)
             } else if (s.mode == PN2_SRC_GROUP_ALL) {
                 b = (int)(R / (unsigned)s.N);
                 n = (int)(R - (unsigned)b * (unsigned)s.N);

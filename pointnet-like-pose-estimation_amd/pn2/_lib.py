@@ -12,8 +12,11 @@ import os
 
 import torch  # noqa: F401  (must be loaded before libpn2.so: shared HIP runtime)
 
+from . import tuning
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PN2_LIB") or os.path.join(_HERE, "libpn2.so")  # PN2_LIB: A/B builds
+# tuning key `lib` (PN2_TUNING=lib=...): an alternative build, for A/B experiments only
+LIB_PATH = tuning.get("lib") or os.path.join(_HERE, "libpn2.so")
 
 _i64 = ctypes.c_int64
 _int = ctypes.c_int
@@ -52,6 +55,8 @@ PATH_SPLIT_BF16 = 2
 PATH_BF16 = 3
 LAYER_NO_RELU = 1
 LINEAR_RELU = 1
+DEVERR_NO_NEIGHBOUR = 1
+DEVERR_INDEX = 2
 
 # name -> (restype, argtypes); every symbol include/pn2.h declares
 SIGNATURES = {
@@ -95,9 +100,13 @@ SIGNATURES = {
     "pn2_sa_mlp_workspace_bytes_bf16": (_i64, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int]),
     "pn2_sa_mlp_max_bf16": (_int, [ctypes.POINTER(SaSrc), ctypes.POINTER(MlpLayer), _int, _int, _vp,
                                    _i64, _vp, _i64, _vp]),
+    "pn2_tuning_get": (_int, [ctypes.c_char_p, ctypes.POINTER(_i64)]),
+    "pn2_tuning_set": (_int, [ctypes.c_char_p, _i64]),
+    "pn2_tuning_keys": (ctypes.c_char_p, []),
+    "pn2_device_errors": (_int, [_int, ctypes.POINTER(ctypes.c_uint32)]),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 _lib = None
 
 
@@ -117,6 +126,7 @@ def load():
         fn.argtypes = args
     if L.pn2_abi_version() != ABI_VERSION:
         raise ImportError("pn2: libpn2.so ABI %d != expected %d" % (L.pn2_abi_version(), ABI_VERSION))
+    tuning.apply_env(L)
     _lib = L
     return L
 
@@ -125,6 +135,34 @@ def check(rc, what):
     if rc != 0:
         msg = load().pn2_last_error().decode(errors="replace")
         raise Pn2Error("%s failed (code %d): %s" % (what, rc, msg))
+
+
+def device_errors(device=None, clear=True):
+    """The device error word (include/pn2.h pn2_device_errors) after the device's queued work:
+    bits DEVERR_*; cleared unless clear=False."""
+    torch.cuda.synchronize(device)
+    prev = torch.cuda.current_device()
+    if device is not None:
+        torch.cuda.set_device(device)
+    try:
+        bits = ctypes.c_uint32(0)
+        check(load().pn2_device_errors(1 if clear else 0, ctypes.byref(bits)), "pn2_device_errors")
+    finally:
+        torch.cuda.set_device(prev)
+    return bits.value
+
+
+def check_device_errors(device=None):
+    """Raise IndexError -- what the reference raises -- when a kernel met an index the reference
+    would have rejected since the last check (a ball-query centroid with no neighbour in its
+    radius, or an out-of-range index_points / grouping index); clears the word."""
+    bits = device_errors(device)
+    if bits & DEVERR_NO_NEIGHBOUR:
+        raise IndexError("pn2: a query_ball_point centroid had no point within its radius; its "
+                         "group is padded with index N, which the reference's index_points "
+                         "rejects (pointnet2_utils.py:85-89, 44)")
+    if bits & DEVERR_INDEX:
+        raise IndexError("pn2: index_points / grouping index out of range [-N, N)")
 
 
 def stream_ptr(device):

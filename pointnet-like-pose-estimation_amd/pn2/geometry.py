@@ -15,15 +15,16 @@ alive and unmodified (same version counter; views share it).  Tensors allocated 
 stream and read on the caller's stream are ``record_stream``-ed there, so the caching allocator
 does not recycle them early.
 
-Opt-in with ``PN2_GEOMETRY_STREAM=1``; by default (and inside graph capture) everything stays
+Opt-in with tuning ``geometry_stream`` = 1 (pn2/tuning.py); by default (and inside graph capture) everything stays
 on the caller's stream.
 """
 import contextlib
-import os
 import threading
 import weakref
 
 import torch
+
+from . import tuning
 
 _streams = {}
 _produced = {}  # data_ptr -> (weakref to owning tensor, version, event)
@@ -32,8 +33,7 @@ _produced = {}  # data_ptr -> (weakref to owning tensor, version, event)
 def enabled():
     # opt-in: on MI355X the overlap it buys (FPS2/BQ2 under MLP1, ~40 us) is about what the
     # cross-stream wait and the CU sharing cost (measured 0.8726 vs 0.8713 ms/step, SSG B=32)
-    return (os.environ.get("PN2_GEOMETRY_STREAM", "0") == "1"
-            and not torch.cuda.is_current_stream_capturing())
+    return bool(tuning.get("geometry_stream")) and not torch.cuda.is_current_stream_capturing()
 
 
 def _stream(device):

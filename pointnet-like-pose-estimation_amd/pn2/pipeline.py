@@ -45,8 +45,6 @@ stream when ``run`` is called.
 """
 import atexit
 import ctypes
-import os
-
 import time
 
 import torch
@@ -55,6 +53,7 @@ from . import _lib
 from . import geometry
 from . import ops
 from . import shard
+from . import tuning
 from .pointnet2_utils import PointNetSetAbstraction, PointNetSetAbstractionMsg
 
 _partitions = {}  # (device, geometry CUs) -> (geometry, compute, tail streams, raw handles)
@@ -123,8 +122,8 @@ def _streams(device, geometry_cus):
         geo = torch.cuda.Stream(dev, priority=min(lo, hi))
         geo2 = torch.cuda.Stream(dev, priority=min(lo, hi))
         main = torch.cuda.Stream(dev)
-        # PN2_TAIL_PRIO=1: the tail (heads) at high priority as well (A/B knob)
-        tail = torch.cuda.Stream(dev, priority=min(lo, hi) if os.environ.get("PN2_TAIL_PRIO") == "1" else 0)
+        # tuning tail_prio = 1: the tail (heads) at high priority as well (A/B)
+        tail = torch.cuda.Stream(dev, priority=min(lo, hi) if tuning.get("tail_prio") else 0)
         main2 = torch.cuda.default_stream(dev)
         for st in (geo, main, tail):
             with torch.cuda.stream(st):
@@ -145,7 +144,10 @@ def _streams(device, geometry_cus):
 
 def _extra_geometry_streams(device, n):
     """n (0 or 1) more high-priority streams for GraphedPipeline(geometry_streams=1+n) (shared
-    CUs; created with the others by _streams)."""
+    CUs; created with the others by _streams).  n = 0 touches no stream: with geometry_cus > 0
+    the shared-CU set would add queues beyond the masked streams'."""
+    if n <= 0:
+        return []
     _streams(device, 0)
     return [_extra[device][0]][:n]
 
@@ -444,7 +446,7 @@ class GraphedPipeline(PipelinedForward):
         self.compute_streams = int(compute_streams)
         # the head graphs get the tail stream while the queues allow it
         self.head_on_tail = (geometry_streams + self.compute_streams + 1 <= 4 and
-                             os.environ.get("PN2_HEADS_ON_COMPUTE", "") != "1")  # A/B knob
+                             not tuning.get("heads_on_compute"))  # A/B
         self.nslots = int(nslots)
         self.gb = gb
         self.ngroups = self.nslots // gb
@@ -466,14 +468,14 @@ class GraphedPipeline(PipelinedForward):
         it, so the group_all layer runs with the head on the tail stream -- beside the next
         batch's wide sa1/sa2 kernels instead of after them.  Only with shared CUs: with
         geometry_cus > 0 the tail stream is masked to the geometry CUs, where a group_all MLP
-        would compete with FPS on a few CUs.  PN2_PIPE_SPLIT=last keeps the old split (A/B).
+        would compete with FPS on a few CUs.  Tuning pipe_split_last = 1 keeps the old split (A/B).
 
         The head graph then reads the split layer's outputs -- sa2's centroids are a static
         output of the group's fps graph -- so the group's next fps replay waits for the head
         (``ev_read`` in ``run``), not only for the sa graph."""
         k = len(self.sas) - 1
         if (k > 0 and getattr(self.sas[k], "group_all", False) and self.geometry_cus <= 0 and
-                os.environ.get("PN2_PIPE_SPLIT", "") != "last"):
+                not tuning.get("pipe_split_last")):
             k -= 1
         return k
 
@@ -670,7 +672,7 @@ class GraphedPipeline(PipelinedForward):
                 ev_fps[s] = geo.record_event()
                 mark(js[0] - first, "geo1", geo)
 
-        drain = int(os.environ.get("PN2_DRAIN_HEADS", "2"))  # see the head stream choice below
+        drain = int(tuning.get("drain_heads"))  # see the head stream choice below
         issued = [0]  # geometry groups issued so far (always in group order: the draw order)
 
         def top_up(force, limit):

@@ -11,16 +11,20 @@ MLP):
   pn2::fps            FPS + gathered centroids + packed (coords, ssq) records
   pn2::ball_query     first-K-in-radius neighbour indices
   pn2::sa_mlp_max_    fused gather -> conv1x1/BN/ReLU chain -> max over neighbours
-(+ per scale for the MSG module).  Hidden activations never leave LDS; the per-layer
-``[B, C, K, S]`` tensors of the reference are never materialised.
+(+ per scale for the MSG module).  Hidden activations stay in registers (the chain kernel) or
+pass through an HBM workspace between the dense-layer launches (group_all layers); the
+per-layer ``[B, C, K, S]`` tensors of the reference are never materialised.
 
 Training (``model.train()`` or autograd through the weights) keeps the reference's semantics
 (batch-statistics BatchNorm, autograd through the MLP and the feature gather): FPS and the ball
 query still run as HIP kernels (they are index ops with no gradient); in train mode the
 grouping and the MLP + max run forward and backward on the training kernels of pn2/train.py
-(csrc/train.hip around library GEMMs).  Eval with autograd enabled (``model.eval()`` without
-``torch.no_grad()``) still runs the fused inference kernels; only inputs that need a gradient,
-or ``eval_autograd()`` (eval-mode fine-tuning), select the torch device formulation.
+(csrc/train.hip around library GEMMs).  As in the reference, an eval-mode forward with
+autograd enabled (``model.eval()`` without ``torch.no_grad()``, parameters requiring grad) is
+differentiable: it runs the torch device formulation.  The fused inference kernels serve
+eval-mode forwards under ``torch.no_grad()`` / ``torch.inference_mode()``, with parameters that
+need no gradient, or inside ``pn2.fused_eval()`` (the mutilthreading/predict_test.py pattern
+made fast: its outputs carry no autograd history).
 
 Device tensors only -- the reference's CPU execution is not re-implemented here.
 """
@@ -58,70 +62,43 @@ def _precision(module):
     return ops.current_precision() if p is None else p
 
 
-_eval_ag = threading.local()
+_fused = threading.local()
+
+
+@contextlib.contextmanager
+def fused_eval(enabled=True):
+    """Within this context (this thread) eval-mode forwards run the fused inference kernels even
+    with autograd enabled (``model.eval()`` without ``torch.no_grad()``, the
+    mutilthreading/predict_test.py pattern): the no_grad bits, no autograd history (a backward
+    through the outputs finds nothing that requires grad).  Outside it such a forward is
+    differentiable, as in the reference."""
+    prev = getattr(_fused, "on", False)
+    _fused.on = bool(enabled)
+    try:
+        yield
+    finally:
+        _fused.on = prev
 
 
 @contextlib.contextmanager
 def eval_autograd(enabled=True):
-    """Within this context (this thread), an eval-mode forward with autograd enabled runs the
-    reference's torch formulation and is differentiable in the weights (eval-mode
-    fine-tuning).  Outside it such a forward runs the fused inference kernels -- the
-    ``model.eval()`` without ``torch.no_grad()`` pattern of mutilthreading/predict_test.py --
-    and a backward through its SA outputs raises instead of leaving the weights' gradients
-    silently missing."""
-    prev = getattr(_eval_ag, "on", False)
-    _eval_ag.on = bool(enabled)
-    try:
+    """Round-2 name kept for callers: eval-mode forwards with autograd enabled are
+    differentiable (the default now); ``enabled=False`` is ``fused_eval()``."""
+    with fused_eval(not enabled):
         yield
-    finally:
-        _eval_ag.on = prev
-
-
-class _InferenceOutput(torch.autograd.Function):
-    """Identity on an eval-mode output of the fused kernels, attached to the module's
-    parameters so that a backward through it fails loudly."""
-
-    @staticmethod
-    def forward(ctx, out, *params):
-        return out.view_as(out)
-
-    @staticmethod
-    def backward(ctx, *grads):
-        raise RuntimeError(
-            "pn2: this output came from an eval-mode forward on the fused inference kernels, "
-            "which have no backward; run the forward under model.train() (training kernels) or "
-            "inside pn2.eval_autograd() (the reference's differentiable formulation)")
 
 
 def _needs_autograd(module, *tensors):
-    """Whether a forward must be differentiable: training mode, or autograd on and either an
-    input that needs a gradient (outputs of another fused eval forward do not) or, inside
-    ``eval_autograd()``, weights that need one."""
+    """Whether a forward must be differentiable: training mode, or autograd on (outside
+    ``fused_eval()``) with an input or a parameter that needs a gradient -- the reference's
+    eval forward is differentiable whenever autograd is."""
     if module.training:
         return True
-    if not torch.is_grad_enabled():
+    if not torch.is_grad_enabled() or getattr(_fused, "on", False):
         return False
-    if any(t is not None and t.requires_grad and not getattr(t, "_pn2_inference", False)
-           for t in tensors):
+    if any(t is not None and t.requires_grad for t in tensors):
         return True
-    return getattr(_eval_ag, "on", False) and any(p.requires_grad for p in module.parameters())
-
-
-def _inference_outputs(module, *outs):
-    """Fused eval outputs under autograd: tie them to the weights through _InferenceOutput (a
-    backward raises) and tag them so the next fused layer does not take them for inputs that
-    need a gradient."""
-    if not torch.is_grad_enabled():
-        return outs
-    params = [p for p in module.parameters() if p.requires_grad]
-    if not params:
-        return outs
-    res = []
-    for o in outs:
-        o = _InferenceOutput.apply(o, *params)
-        o._pn2_inference = True
-        res.append(o)
-    return tuple(res)
+    return any(p.requires_grad for p in module.parameters())
 
 
 def _pack_chain(convs, bns, cache, rot0, xyz=0, xyz_first=True):
@@ -271,7 +248,7 @@ class PointNetSetAbstraction(nn.Module):
             ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_ALL, pts, feat, None, None, wts, als, bes, cins,
                             splits, _precision(self))
             new_points = torch.zeros(B, C, 1, device=dev, dtype=torch.float32)
-            return _inference_outputs(self, new_points, out.view(B, 1, cout).permute(0, 2, 1))
+            return new_points, out.view(B, 1, cout).permute(0, 2, 1)
         S, K = self.point_number, self.sample_number
         pre = geometry.take(self, pts)  # FPS (+ ball query) precomputed by pn2.pipeline
         if pre is not None:
@@ -285,8 +262,7 @@ class PointNetSetAbstraction(nn.Module):
         out = torch.empty(B * S, cout, device=dev, dtype=torch.float32)
         ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
                         cins, splits, _precision(self), cnt=cnt)
-        return _inference_outputs(self, new_points.permute(0, 2, 1),
-                                  out.view(B, S, cout).permute(0, 2, 1))
+        return new_points.permute(0, 2, 1), out.view(B, S, cout).permute(0, 2, 1)
 
     def _forward_autograd(self, points, feature):
         pts = points.permute(0, 2, 1)
@@ -360,8 +336,7 @@ class PointNetSetAbstractionMsg(nn.Module):
             ops.sa_mlp_max_direct(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
                             new_points, idx, wts, als, bes, cins, splits, prec, cnt=cnt)
             col += cout
-        return _inference_outputs(self, new_points.permute(0, 2, 1),
-                                  out.view(B, S, total).permute(0, 2, 1))
+        return new_points.permute(0, 2, 1), out.view(B, S, total).permute(0, 2, 1)
 
     def _forward_autograd(self, points, feature):
         pts = points.permute(0, 2, 1)

@@ -85,23 +85,29 @@ def all_gather_rows(local, group=None, sizes=None):
     GPU tensors, gloo on CPU ones).
 
     Shards may be uneven (``shard_range`` gives the remainder to the first ranks).  The row
-    counts come from `sizes`, else from the enclosing ``batch_shard`` (global batch -> every
-    rank's ``shard_range``), else from one extra all_gather of the counts.  Every rank's rows are
-    padded to the largest shard for the one fixed-size collective and trimmed after it."""
+    counts come from `sizes`: a list, or ``"shard"`` -- every rank's ``shard_range`` of the
+    enclosing ``batch_shard``'s global batch (for per-cloud tensors of the shard, e.g. the
+    logits: no extra collective) -- or, by default, from one extra all_gather of the counts
+    (any row counts).  The choice must be the same on every rank (it decides which collectives
+    run).  Every rank's rows are padded to the largest count for the one fixed-size collective
+    and trimmed after it."""
     if not dist.is_available() or not dist.is_initialized():
         return local
     world = dist.get_world_size(group)
     if world == 1:
         return local
     local = local.contiguous()
-    if sizes is None:
+    if isinstance(sizes, str):
+        if sizes != "shard":
+            raise ValueError("all_gather_rows: sizes must be a list, 'shard' or None")
         spec = getattr(_state, "spec", None)
-        if spec is not None and group is None:
-            sizes = shard_sizes(spec[0], world)
-            if sizes[dist.get_rank()] != local.shape[0]:
-                raise ValueError("all_gather_rows: %d rows on rank %d, batch_shard(%d) gives %d"
-                                 % (local.shape[0], dist.get_rank(), spec[0],
-                                    sizes[dist.get_rank()]))
+        if spec is None:
+            raise ValueError("all_gather_rows(sizes='shard') outside batch_shard")
+        sizes = shard_sizes(spec[0], world)
+        if sizes[dist.get_rank(group)] != local.shape[0]:
+            raise ValueError("all_gather_rows: %d rows on rank %d, batch_shard(%d) gives %d"
+                             % (local.shape[0], dist.get_rank(group), spec[0],
+                                sizes[dist.get_rank(group)]))
     if sizes is None:
         n = torch.tensor([local.shape[0]], dtype=torch.long, device=local.device)
         ns = torch.empty(world, dtype=torch.long, device=local.device)

@@ -1,0 +1,97 @@
+"""Tuning of the launch choices -- for A/B experiments and tests, not for users.
+
+The product path reads one environment variable, once, at import:
+
+    PN2_TUNING="key=value,key=value,..."
+
+Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_set``:
+``mlp_f32``, ``chain_prepass``, ``compact``, ``compact_pool``, ``compact_stages``,
+``bq_waves``, ``fps_threads``, ``fps_ppt``, ``dense_maxntc``, ``dense_minwg``,
+``dense_wide_minwg``) and these host-side ones:
+
+    lib              path of an alternative libpn2.so build (A/B builds)
+    tail_prio        1: the pipeline's tail stream at high priority
+    heads_on_compute 1: the pipeline's heads on the compute streams, no tail stream
+    pipe_split_last  1: the pipeline's compute/tail split after the last SA layer
+    drain_heads      how many final batches of a pipelined run take their heads on their own
+                     compute streams (default 2)
+    geometry_stream  1: the eager forward runs layer i+1's FPS + ball query on a side stream
+
+Unknown keys are an error.  ``override(**kw)`` changes keys for the duration of a ``with``
+block (tests).  Every default is the measured best.
+"""
+import contextlib
+import os
+
+HOST_DEFAULTS = {
+    "lib": "",
+    "tail_prio": 0,
+    "heads_on_compute": 0,
+    "pipe_split_last": 0,
+    "drain_heads": 2,
+    "geometry_stream": 0,
+}
+
+
+def _parse(text):
+    out = {}
+    for item in filter(None, (t.strip() for t in text.split(","))):
+        if "=" not in item:
+            raise ValueError("PN2_TUNING: expected key=value, got %r" % item)
+        k, v = (s.strip() for s in item.split("=", 1))
+        out[k] = v if k == "lib" else int(v)
+    return out
+
+
+_ENV = _parse(os.environ.get("PN2_TUNING", ""))
+_host = dict(HOST_DEFAULTS)
+_host.update({k: v for k, v in _ENV.items() if k in HOST_DEFAULTS})
+
+
+def get(key):
+    """A host-side key's value (kernel keys: ``kernel(key)``)."""
+    return _host[key]
+
+
+def kernel(key):
+    """A kernel-selection parameter's current value in the loaded library."""
+    import ctypes
+    from . import _lib
+    v = ctypes.c_int64(0)
+    _lib.check(_lib.load().pn2_tuning_get(key.encode(), ctypes.byref(v)), "pn2_tuning_get")
+    return v.value
+
+
+def _set_kernel(L, key, value):
+    if L.pn2_tuning_set(key.encode(), int(value)) != 0:
+        raise ValueError("pn2 tuning: %s" % L.pn2_last_error().decode(errors="replace"))
+
+
+def apply_env(L):
+    """Apply PN2_TUNING's kernel keys to the just-loaded library L (called by _lib.load)."""
+    for k, v in _ENV.items():
+        if k not in HOST_DEFAULTS:
+            _set_kernel(L, k, v)
+
+
+@contextlib.contextmanager
+def override(**kw):
+    """Change tuning keys (host-side or kernel) within a ``with`` block, then restore them."""
+    from . import _lib
+    L = _lib.load()
+    saved = []
+    try:
+        for k, v in kw.items():
+            if k in HOST_DEFAULTS:
+                saved.append((k, _host[k], True))
+                _host[k] = v
+            else:
+                saved.append((k, kernel(k), False))
+                _set_kernel(L, k, v)
+        yield
+    finally:
+        for k, v, host in reversed(saved):
+            if host:
+                _host[k] = v
+            else:
+                _set_kernel(L, k, v)

@@ -49,20 +49,19 @@ def _oracle_layers(convs, bns):
 
 @pytest.mark.parametrize("path", ["chain", "chain_noprepass", "f32"])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_sa_mlp_vs_oracle(case, path, monkeypatch):
+def test_sa_mlp_vs_oracle(case, path):
     """chain: default dispatch (wide first layers take the per-point layer-0 pre-pass, cases 1,
-    6); chain_noprepass: PN2_CHAIN_PREPASS=0 (layer 0 on the gathered rows); f32: fp32 MFMA."""
+    6); chain_noprepass: tuning chain_prepass = 0 (layer 0 on the gathered rows); f32: fp32
+    MFMA (tuning mlp_f32 = 1)."""
+    from pn2 import tuning
+    with tuning.override(mlp_f32=int(path == "f32"), chain_prepass=int(path != "chain_noprepass")):
+        _sa_mlp_vs_oracle(case, path)
+
+
+def _sa_mlp_vs_oracle(case, path):
     import pn2
     from pn2 import _lib
     C, D, K, S, N, mlp, msg, chain_ok = CASES[case]
-    if path == "f32":
-        monkeypatch.setenv("PN2_MLP_PATH", "f32")
-    else:
-        monkeypatch.delenv("PN2_MLP_PATH", raising=False)
-    if path == "chain_noprepass":
-        monkeypatch.setenv("PN2_CHAIN_PREPASS", "0")
-    else:
-        monkeypatch.delenv("PN2_CHAIN_PREPASS", raising=False)
     B, radius = 2, 0.35
     pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 100 + case)
     gen = torch.Generator().manual_seed(200 + case)
@@ -142,7 +141,7 @@ COMPACT = [
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("case", range(len(COMPACT)))
-def test_compact_neighbourhoods_bit_exact(case, prec, monkeypatch):
+def test_compact_neighbourhoods_bit_exact(case, prec):
     """Computing only each group's distinct rows (8-row units, the padding repeats of the first
     neighbour dropped) gives the bits of the full K rows per group: every row's MLP is
     computed the same way, and the max is the same without repeats.  Covers K % 8 != 0, groups
@@ -150,9 +149,9 @@ def test_compact_neighbourhoods_bit_exact(case, prec, monkeypatch):
     group, MSG, the pose layout, groups past the LDS pool rows, and bf16; the fp32 result also
     against the float64 oracle."""
     import pn2
+    from pn2 import tuning
     C, D, K, S, N, radius, mlp, msg = COMPACT[case]
-    if case >= 7:
-        monkeypatch.setenv("PN2_COMPACT_KS", "3")
+    stages = 3 if case >= 7 else 2
     B = 3
     pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 500 + case)
     gen = torch.Generator().manual_seed(600 + case)
@@ -171,9 +170,9 @@ def test_compact_neighbourhoods_bit_exact(case, prec, monkeypatch):
     outs = {}
     chainable = K in (8, 16) or K % 32 == 0
     for mode in ("0", "1") if (chainable or prec == "fp32") else ("1",):
-        monkeypatch.setenv("PN2_COMPACT", mode)
         torch.manual_seed(77)
-        with torch.no_grad(), pn2.mlp_precision(prec):
+        with torch.no_grad(), pn2.mlp_precision(prec), \
+                tuning.override(compact=int(mode), compact_stages=stages):
             outs[mode] = sa(x, f)[1].cpu().numpy()
     if chainable:  # else the full-row launch is not the chain kernel (no bf16 kernel at all)
         np.testing.assert_array_equal(outs["1"].view(np.uint32), outs["0"].view(np.uint32))
@@ -205,17 +204,17 @@ GROUP_ALL = [
 
 @pytest.mark.parametrize("path", ["split", "f32", "wide"])
 @pytest.mark.parametrize("case", range(len(GROUP_ALL)))
-def test_group_all_vs_oracle(case, path, monkeypatch):
+def test_group_all_vs_oracle(case, path):
+    from pn2 import tuning
+    # wide: the 256 x 128 (8-wave) dense tiles of large layers, at a small size
+    with tuning.override(mlp_f32=int(path == "f32"), dense_wide_minwg=1 if path == "wide" else 512):
+        _group_all_vs_oracle(case, "split" if path == "wide" else path)
+
+
+def _group_all_vs_oracle(case, path):
     import pn2
     from pn2 import _lib
     C, D, N, mlp, split_ok = GROUP_ALL[case]
-    if path == "f32":
-        monkeypatch.setenv("PN2_MLP_PATH", "f32")
-    else:
-        monkeypatch.delenv("PN2_MLP_PATH", raising=False)
-    if path == "wide":  # the 256 x 128 (8-wave) dense tiles of large layers, at a small size
-        monkeypatch.setenv("PN2_DENSE_WIDE_MINWG", "1")
-        path = "split"
     B = 3
     pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 400 + case)
     feat = torch.randn(B, N, D, generator=torch.Generator().manual_seed(500 + case)) if D else None

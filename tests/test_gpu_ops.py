@@ -165,3 +165,54 @@ def test_fps_stress_size_vs_oracle():
         want = oracle.farthest_point_sample(p, S, start)
         idx = torch.ops.pn2.fps(_to_dev_view(p), S, start.to(DEV))[0]
         np.testing.assert_array_equal(idx.cpu().numpy(), want)
+
+
+def test_no_neighbour_centroids_flagged_not_read_out_of_bounds():
+    """Clouds on a millimetre scale: the -2ab + a^2 + b^2 cancellation puts some centroids'
+    distance to themselves above a small r^2, so they have no neighbour.  The reference pads
+    their rows with index N (pointnet2_utils.py:85-89) and its index_points then raises
+    IndexError.  Here query_ball_point returns the same N-padded rows (bit-exact vs the
+    oracle), the SA kernels stay inside the cloud (finite outputs), and
+    pn2.check_device_errors() raises the reference's IndexError -- once (the word clears)."""
+    import pn2
+    pn2.check_device_errors()  # nothing pending from earlier tests
+    B, N, S, K, r = 2, 1024, 512, 32, 0.01
+    pts = cases.cloud("uniform3", B, N, 3) * 1000.0
+    torch.manual_seed(0)
+    start = torch.randint(0, N, (B,))
+    ps = pts.permute(0, 2, 1).contiguous().permute(0, 2, 1)
+    ctr = oracle.index_points(ps, oracle.farthest_point_sample(ps, S, start))
+    want = oracle.query_ball_point(r, K, ps, ctr)
+    assert (want[:, :, 0] == N).sum() > 0  # the case under test exists
+    x = pts.permute(0, 2, 1).contiguous().to(DEV)
+    got = pn2.query_ball_point(r, K, x.permute(0, 2, 1), torch.from_numpy(ctr).to(DEV))
+    np.testing.assert_array_equal(got.cpu().numpy(), want)
+    with pytest.raises(IndexError, match="no point within its radius"):
+        pn2.check_device_errors()
+    pn2.check_device_errors()  # cleared
+    torch.manual_seed(1)
+    sa = pn2.PointNetSetAbstraction(S, K, r, 3, [64, 64, 128]).to(DEV).eval()
+    with torch.no_grad():
+        _, f = sa(x, None)
+    assert torch.isfinite(f).all()
+    with pytest.raises(IndexError):
+        pn2.check_device_errors()
+
+
+def test_index_points_out_of_range_is_nan_and_flagged():
+    """torch's index rule: -N <= n < 0 counts from the end; outside [-N, N) the reference raises
+    IndexError -- here the element is NaN and check_device_errors() raises it."""
+    import pn2
+    pn2.check_device_errors()
+    pts = torch.randn(2, 16, 3, device=DEV)
+    idx = torch.tensor([[0, -1, 5], [15, -16, 3]], device=DEV)
+    got = pn2.index_points(pts, idx)
+    b = torch.arange(2, device=DEV)[:, None]
+    torch.testing.assert_close(got, pts[b, idx], rtol=0, atol=0)
+    pn2.check_device_errors()
+    bad = torch.tensor([[0, 16, 1], [-17, 2, 3]], device=DEV)
+    got = pn2.index_points(pts, bad)
+    assert torch.isnan(got[0, 1]).all() and torch.isnan(got[1, 0]).all()
+    assert torch.equal(got[0, 0], pts[0, 0])
+    with pytest.raises(IndexError, match="out of range"):
+        pn2.check_device_errors()

@@ -170,7 +170,7 @@ def test_stress_config_geometry():
 
 
 @pytest.mark.parametrize("head", ["ClsSSG", "ClsMSG"])
-def test_geometry_stream_matches_single_stream(head, monkeypatch):
+def test_geometry_stream_matches_single_stream(head):
     """FPS/ball query on the geometry stream (overlapping the previous layer's MLP) give the
     same bits as running everything on the caller's stream -- over back-to-back forwards whose
     temporaries churn the caching allocator, with the inputs freed right after each launch."""
@@ -193,13 +193,14 @@ def test_geometry_stream_matches_single_stream(head, monkeypatch):
         torch.cuda.synchronize()
         return [o.cpu().numpy() for o in outs]
 
-    monkeypatch.setenv("PN2_GEOMETRY_STREAM", "0")
-    want = run()
-    monkeypatch.setenv("PN2_GEOMETRY_STREAM", "1")
-    for _ in range(2):
-        got = run()
-        for g, w in zip(got, want):
-            np.testing.assert_array_equal(g, w)
+    from pn2 import tuning
+    with tuning.override(geometry_stream=0):
+        want = run()
+    with tuning.override(geometry_stream=1):
+        for _ in range(2):
+            got = run()
+            for g, w in zip(got, want):
+                np.testing.assert_array_equal(g, w)
 
 
 @pytest.mark.parametrize("head", ["ClsSSG", "ClsMSG", "RotationSSG"])
@@ -256,8 +257,8 @@ def test_pipelined_forward_matches_eager(head, tail):
     """pn2.pipeline.PipelinedForward (FPS of batch i+1 on its own CUs while batch i runs) returns
     the eager forwards' results for a sequence of batches -- including a sharded call -- and
     leaves the CPU generator where the eager sequence leaves it.  Every SA output (the l3
-    feature) is bit-identical; the head's Linear layers go through torch's BLAS, which may pick
-    another GEMM kernel on the CU-restricted stream, so logits are held to 1e-6 relative."""
+    feature) and the logits are bit-identical (the FC tail runs on pn2's row kernel, which
+    computes every row the same way on any stream)."""
     from pn2 import heads as H
     from pn2 import shard
     from pn2.pipeline import PipelinedForward
@@ -293,7 +294,7 @@ def test_pipelined_forward_matches_eager(head, tail):
     for g, w in zip(feats, want_f):
         np.testing.assert_array_equal(g, w)
     for g, w in zip(got, want):
-        np.testing.assert_allclose(g, w, rtol=1e-6, atol=1e-6 * float(np.abs(w).max()))
+        np.testing.assert_array_equal(g, w)
 
 
 @pytest.mark.parametrize("head,tail", [("ClsSSG", True), ("ClsSSG", False), ("ClsMSG", True),
@@ -303,8 +304,8 @@ def test_graphed_pipeline_matches_eager(head, tail):
     compute and tail streams, two slots) returns the eager forwards' results for a sequence of
     batches -- the first batch eager, the rest replayed through both slots twice, under
     shard.batch_shard -- and walks the CPU generator exactly as the eager sequence does.  The
-    cls heads return the last SA feature (l3f), held bit-identical; logits to 1e-6 relative
-    (the head's torch BLAS may pick another GEMM on a CU-restricted stream).  A second run()
+    cls heads return the last SA feature (l3f); every output is held bit-identical (the FC tail
+    runs on pn2's row kernel).  A second run()
     replays without recapturing; an in-place BN change recaptures."""
     from pn2 import heads as H
     from pn2 import shard
@@ -346,8 +347,7 @@ def test_graphed_pipeline_matches_eager(head, tail):
     for i, (g, w) in enumerate(zip(got, want)):
         assert len(g) == len(w)
         for k, (a, b) in enumerate(zip(g, w)):
-            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * float(np.abs(b).max()),
-                                       err_msg="output %d of batch %d" % (k, i))
+            np.testing.assert_array_equal(a, b, err_msg="output %d of batch %d" % (k, i))
 
     # a parameter change recaptures and still matches eager
     next(b for n, b in model.sa1.named_buffers() if n.endswith("running_mean")).add_(0.25)
@@ -359,7 +359,7 @@ def test_graphed_pipeline_matches_eager(head, tail):
     assert gp._slots is not slots
     for g, w in zip(got2, want2):
         for a, b in zip(g, w):
-            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * float(np.abs(b).max()))
+            np.testing.assert_array_equal(a, b)
 
 
 @pytest.mark.parametrize("layout", ["contig", "tview"])
@@ -368,7 +368,7 @@ def test_graphed_pipeline_multihead_matches_eager(layout):
     pn2.pipeline.MultiHead: the FPS chain covers both heads (a group_all layer ends a head's
     chain, the next head restarts from the input; the heads' first FPS run as one launch over
     the repeated input), draws in the order separate eager calls take them, and every output
-    matches those calls (logits to 1e-6: head BLAS on another stream).  tview: the input is the
+    matches those calls bit for bit.  tview: the input is the
     transpose view of [B, N, C] storage (the scripts' layout), which the repeated copy keeps."""
     from pn2 import heads as H
     from pn2 import shard
@@ -395,8 +395,7 @@ def test_graphed_pipeline_multihead_matches_eager(layout):
     np.testing.assert_array_equal(torch.randint(0, 1 << 30, (4,)).numpy(), rng_want.numpy())
     for i, (g, w) in enumerate(zip(got, want)):
         for k, (a, b) in enumerate(zip(g, w)):
-            np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6 * float(np.abs(b).max()),
-                                       err_msg="head %d of batch %d" % (k, i))
+            np.testing.assert_array_equal(a, b, err_msg="head %d of batch %d" % (k, i))
 
 
 @pytest.mark.parametrize("compute_streams,geometry_streams", [(1, 2), (2, 1), (2, 2)])
@@ -437,11 +436,13 @@ def test_graphed_pipeline_delayed_tail_matches_eager(compute_streams, geometry_s
         np.testing.assert_array_equal(g, w, err_msg="l3f of batch %d" % i)
 
 
-def test_eval_without_no_grad_takes_fused_path():
-    """model.eval() without torch.no_grad() (mutilthreading/predict_test.py:44-63) runs the
-    fused split-bf16 kernels and gives the no_grad bits; a backward through those outputs raises
-    instead of silently leaving the SA weights without gradients; inside pn2.eval_autograd() the
-    same forward is the differentiable torch formulation (eval-mode fine-tuning)."""
+def test_eval_with_autograd_is_differentiable():
+    """model.eval() without torch.no_grad() (mutilthreading/predict_test.py:44-63) is
+    differentiable, as the reference's eval forward is: the torch device formulation, within the
+    feature tolerance of the no_grad (fused) run, with weight gradients after a backward.
+    Inside pn2.fused_eval() the same forward runs the fused split-bf16 kernels and gives the
+    no_grad bits -- logits included (the FC tail takes the fused row kernel too) -- with no
+    autograd history."""
     import pn2
     from pn2 import _lib
     from pn2 import heads as H
@@ -454,17 +455,17 @@ def test_eval_without_no_grad_takes_fused_path():
     with torch.no_grad():
         want = model(x)
     torch.manual_seed(1)
-    got = model(x)  # autograd on, parameters require grad
-    assert _lib.load().pn2_sa_mlp_last_path() == _lib.PATH_SPLIT_BF16
-    np.testing.assert_array_equal(got[1].detach().cpu().numpy(), want[1].cpu().numpy())
-    np.testing.assert_allclose(got[0].detach().cpu().numpy(), want[0].cpu().numpy(),
-                               rtol=1e-5, atol=1e-6)
-    with pytest.raises(RuntimeError, match="fused inference kernels"):
-        got[0].sum().backward()
+    got = model(x)  # autograd on, parameters require grad: the differentiable formulation
+    assert got[0].requires_grad
+    got[0].sum().backward()
+    assert model.sa1.mlp_convs[0].weight.grad is not None
+    assert model.sa3.mlp_convs[2].weight.grad is not None
+    assert_feat_close(got[1].detach().cpu().numpy(), want[1].cpu().numpy())
     model.zero_grad()
     torch.manual_seed(1)
-    with pn2.eval_autograd():
-        ft = model(x)
-    ft[0].sum().backward()
-    assert model.sa1.mlp_convs[0].weight.grad is not None
-    assert_feat_close(ft[1].detach().cpu().numpy(), want[1].cpu().numpy())
+    with pn2.fused_eval():
+        fz = model(x)
+    assert _lib.load().pn2_sa_mlp_last_path() == _lib.PATH_SPLIT_BF16
+    assert not fz[0].requires_grad
+    for a, b in zip(fz, want):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())

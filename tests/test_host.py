@@ -104,7 +104,11 @@ def _gloo_worker(rank, world, port, out, B=8):
     with shard.batch_shard(B, lo):
         starts = shard.draw_start(hi - lo, 100)
         local = torch.stack([starts.double(), torch.full((hi - lo,), float(rank), dtype=torch.float64)], 1)
-        got_spec = shard.all_gather_rows(local)  # row counts from batch_shard
+        got_spec = shard.all_gather_rows(local, sizes="shard")  # row counts from batch_shard
+        # a tensor that is not per-cloud (one summary row per rank) inside batch_shard: the
+        # default gathers the row counts
+        summ = shard.all_gather_rows(torch.full((1, 2), float(rank), dtype=torch.float64))
+        assert summ[:, 0].tolist() == [float(r) for r in range(world)]
     got = shard.all_gather_rows(local)  # row counts gathered from the ranks
     got_sizes = shard.all_gather_rows(local, sizes=shard.shard_sizes(B, world))
     if rank == 0:
@@ -138,6 +142,55 @@ def test_gloo_all_gather_and_rng_parity(B, world):
         assert got.shape == (B, 2)
         np.testing.assert_array_equal(got[:, 0].astype(np.int64), want)
         np.testing.assert_array_equal(got[:, 1], owner)
+
+
+BENCH = os.path.join(os.path.dirname(PKG), "bench.py")
+
+
+@pytest.mark.parametrize("config,gpus", [("ssg", 2), ("pose", 3)])
+def test_bench_launcher_plumbing(config, gpus):
+    """`bench.py --gpus N` (no torchrun) starts N ranks itself with the torchrun environment;
+    --plumbing-check runs their gloo group, shard split and uneven all_gather on the CPU (pose:
+    the global B=64 over 3 ranks is uneven).  The JSON line must report n_gpus == N."""
+    import json
+    import subprocess
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(gpus), "--config", config,
+                        "--plumbing-check"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["plumbing_check"] is True
+    assert line["n_gpus"] == gpus
+    assert line["global_batch"] == (64 if config == "pose" else 32 * gpus)
+
+
+def test_bench_rejects_world_mismatch():
+    """Under a launcher, --gpus must equal WORLD_SIZE (no silent one-rank run)."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--plumbing-check"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_count_gpus_without_hip(monkeypatch, tmp_path):
+    """The launcher's parent counts GPUs from the KFD topology and the visibility variables,
+    never through HIP (a parent that initialised HIP before forking its ranks is the hazard)."""
+    sys.path.insert(0, os.path.dirname(PKG))
+    import bench
+    topo = tmp_path / "nodes"
+    for i, simds in enumerate([0, 256, 256, 256]):  # node 0: the CPU
+        d = topo / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text("cpu_cores_count 0\nsimd_count %d\n" % simds)
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    assert bench.count_gpus(str(topo)) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    assert bench.count_gpus(str(topo)) == 2
+    assert bench.count_gpus(str(tmp_path / "absent")) == 0
 
 
 def shard_ranges(B, world):

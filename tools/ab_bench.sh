@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B: bench + kernel stats for the default libpn2.so and each pn2/var/*.so (PN2_LIB override).
+# A/B: bench + kernel stats for the default libpn2.so and each pn2/var/*.so (PN2_TUNING=lib=... override).
 # Every GPU step has its own time limit; the first failure ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 ARGS="${BENCH_ARGS:-}"
 for lib in default pointnet-like-pose-estimation_amd/pn2/var/*.so; do
   tag=$(basename $lib .so)
-  if [ $lib = default ]; then unset PN2_LIB; else export PN2_LIB=$PWD/$lib; fi
+  if [ $lib = default ]; then unset PN2_TUNING; else export PN2_TUNING=lib=$PWD/$lib; fi
   for i in 1 2; do
     timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline $ARGS > $OUT/bench_${tag}_$i.log 2>&1 || exit $?
     python - "$tag" $OUT/bench_${tag}_$i.log <<'PY'

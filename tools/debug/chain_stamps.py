@@ -1,5 +1,5 @@
 """Per-workgroup timeline of the SA chain kernel (diagnostic build, tools/debug/build_stamps.sh):
-PN2_LIB=.../pn2/var/stamps.so python tools/debug/chain_stamps.py
+PN2_TUNING=lib=.../pn2/var/stamps.so python tools/debug/chain_stamps.py
 Runs the SSG B=32 N=1024 sa1 and sa2 layers once each (eager, after warm-up) and prints, per
 layer: kernel span, workgroups that did work / left early, percentiles of each phase
 (setup = entry -> BN staged, layer 0 incl. gather, layer 1, layer 2 + pooling, write-out)
@@ -78,12 +78,12 @@ def main():
         model.sa2(l1p, l1f)
         st2 = stamps()
         report("sa2 (pre-pass, KB0M=-1)", st2, 32 * 128 * 64 // 128)
-        # the compact variant of sa2 (PN2_COMPACT=1: distinct rows only, 8-row units)
+        # the compact variant of sa2 (compact: distinct rows only, 8-row units)
         os.environ["PN2_COMPACT"] = "1"
         model.sa2(l1p, l1f)
         model.sa2(l1p, l1f)
         st3 = stamps()
-        report("sa2 compact (PN2_COMPACT=1)", st3, 32 * 128 * 64 // 128)
+        report("sa2 compact", st3, 32 * 128 * 64 // 128)
         del os.environ["PN2_COMPACT"]
 
 

@@ -1,5 +1,5 @@
 """Per-workgroup timeline of the dense layer kernel (diagnostic build,
-tools/debug/build_dense_stamps.sh): PN2_LIB=.../pn2/var/dstamps.so python tools/debug/dense_stamps.py
+tools/debug/build_dense_stamps.sh): PN2_TUNING=lib=.../pn2/var/dstamps.so python tools/debug/dense_stamps.py
 Runs one eager SSG B=32 N=1024 forward after warm-up; the last dense launch of it is sa3's
 512 -> 1024 layer (group_all, pooled over the 128 points of a cloud); CONFIG=pose: translation_ssg's
 sa2 512 -> 1024 layer at B=64 (GRID=1024 wide tiles, NST=8).  Prints the spread of

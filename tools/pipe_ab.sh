@@ -12,5 +12,5 @@ while IFS='|' read -r tag envs args; do
   done
 done <<< "${VARIANTS:-base|X=1|
 slots4|X=1|--slots 4
-splitlast|PN2_PIPE_SPLIT=last|
-splitlast4|PN2_PIPE_SPLIT=last|--slots 4}"
+splitlast|PN2_TUNING=pipe_split_last=1|
+splitlast4|PN2_TUNING=pipe_split_last=1|--slots 4}"

@@ -15,5 +15,5 @@ run() {  # tag, env assignments..., -- bench args...
   done
 }
 run default X=1 --
-run heads_compute PN2_HEADS_ON_COMPUTE=1 --
+run heads_compute PN2_TUNING=heads_on_compute=1 --
 run no_tail X=1 -- --no-tail

@@ -7,7 +7,7 @@ for r in 1 2 3; do
   for v in 0 1; do
     for k in 20 100; do
       w=5; [ $k = 100 ] && w=10
-      PN2_TAIL_PRIO=$v timeout -k 10 300 python bench.py --steps $k --warmup $w --no-cpu-baseline --no-kernel-timer > gpurun_out/ab/t_$v.log 2>&1 || { echo "$v rc=$?"; exit 1; }
+      PN2_TUNING=tail_prio=$v timeout -k 10 300 python bench.py --steps $k --warmup $w --no-cpu-baseline --no-kernel-timer > gpurun_out/ab/t_$v.log 2>&1 || { echo "$v rc=$?"; exit 1; }
       grep '^{' gpurun_out/ab/t_$v.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('tail_prio=$v K=$k', d['value'], d['ms_per_step'])"
     done
   done
