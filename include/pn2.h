@@ -205,6 +205,10 @@ typedef struct pn2_sa_src {
     const int32_t *cnt;                   /* [B,S] distinct neighbours per group
                                              (pn2_ball_query_cnt_f32), or NULL: group
                                              modes then compute only those rows          */
+    float *zero_out; int64_t zero_count;  /* side job, or NULL: zero_count floats to zero
+                                             (group_all's new_points, the reference's
+                                             torch.zeros(B,1,C), pointnet2_utils.py:136),
+                                             done by one of the call's launches          */
 } pn2_sa_src;
 
 /* Bytes of workspace pn2_sa_mlp_max_f32 needs for this layer chain: 0 when the chain runs as
@@ -300,6 +304,25 @@ int pn2_bn_relu_backward_f32(const float *Y, int64_t M, int64_t C, int64_t ld, c
 int pn2_linear_rows_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const float *W,
                         const float *bias, float *out, int64_t ldo, int64_t N, int flags,
                         void *stream);
+
+/* ---- the PointNet++ heads' eval FC tail in two launches: fc1 + bn1 + ReLU, fc2 + bn2 + ReLU,
+ * fc3 (BN folded into W / bias on the host; dropout is the identity in eval), and with
+ * PN2_TAIL_LOGSOFTMAX the classifiers' log_softmax over the N3 logits and the first argmax of
+ * each row -- pointnet2_cls_ssg.py:31-38 (F.log_softmax(x, -1), x.data.max(1)[1]), the same
+ * tails of pointnet2_cls_msg.py, rotation_ssg.py, translation_ssg.py, sign_ssg.py.  x [B][K]
+ * (row stride ldx), W1 [N1][K], W2 [N2][N1], W3 [N3][N2] row-major; out [B][N3] (row stride
+ * ldo): the log-probabilities with the flag, else the fc3 outputs; argmax [B] int64 or NULL.
+ * fc1 and fc2 elements are computed as pn2_linear_rows_f32 computes them; each fc3 element is
+ * a sequential float32 fma chain over k.  B * N3 <= 4096.  workspace:
+ * pn2_fc_tail_workspace_bytes(B, N1, N2) bytes, 16-byte aligned (it holds an arrival ticket
+ * the first launch zeroes; calls sharing a workspace must be stream-ordered). */
+#define PN2_TAIL_LOGSOFTMAX 1
+int64_t pn2_fc_tail_workspace_bytes(int64_t B, int64_t N1, int64_t N2);
+int pn2_fc_tail_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const float *W1,
+                    const float *b1, int64_t N1, const float *W2, const float *b2, int64_t N2,
+                    const float *W3, const float *b3, int64_t N3, int flags, float *out,
+                    int64_t ldo, int64_t *argmax, void *workspace, int64_t workspace_bytes,
+                    void *stream);
 
 /* Which kernel family served this thread's last successful pn2_sa_mlp_max_* call:
  * PN2_PATH_F32 (fp32 MFMA kernels), PN2_PATH_SPLIT_BF16 (split-bf16 chain / dense kernels) or

@@ -42,13 +42,13 @@ __device__ __forceinline__ void lin_reduce_step(float *a, int lane) {
     }
 }
 
+// one workgroup's block: output features blockIdx.x * kLinRows.., rows blockIdx.y * BT..
 template <int BT>
-__global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float *__restrict__ x, int64_t ldx,
-                                                                     int B, int64_t K,
-                                                                     const float *__restrict__ W,
-                                                                     const float *__restrict__ bias,
-                                                                     float *__restrict__ out, int64_t ldo,
-                                                                     int64_t N, int relu, int vec) {
+__device__ __forceinline__ void linear_rows_block(const float *__restrict__ x, int64_t ldx, int B, int64_t K,
+                                                  const float *__restrict__ W,
+                                                  const float *__restrict__ bias,
+                                                  float *__restrict__ out, int64_t ldo, int64_t N,
+                                                  int relu, int vec) {
     constexpr int kLinRows = lin_rows<BT>();
     const int lane = threadIdx.x & 63;
     // row block blockIdx.y: every output element is computed the same way whatever B is (the
@@ -135,6 +135,97 @@ __global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float
     }
 }
 
+template <int BT>
+__global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float *__restrict__ x, int64_t ldx,
+                                                                     int B, int64_t K,
+                                                                     const float *__restrict__ W,
+                                                                     const float *__restrict__ bias,
+                                                                     float *__restrict__ out, int64_t ldo,
+                                                                     int64_t N, int relu, int vec,
+                                                                     unsigned *zero_word) {
+    // side job: reset the next launch's arrival ticket (fc_tail), published by stream order
+    if (zero_word && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *zero_word = 0u;
+    linear_rows_block<BT>(x, ldx, B, K, W, bias, out, ldo, N, relu, vec);
+}
+
+// ---- the heads' FC tail, second half: fc2 (+ folded BN, ReLU) over the grid as
+// linear_rows_kernel, then the workgroup that finishes last computes fc3 for every row and, with
+// PN2_TAIL_LOGSOFTMAX, log_softmax and the first argmax of each row (pointnet2_cls_ssg.py:36-38:
+// F.log_softmax(x, -1) and x.data.max(1)[1]).  fc3 element (b, n) is one thread's sequential
+// fma chain over k (the same whatever the row count: sharded batches stay bit-identical).
+// Hand-off: every workgroup's y2 stores -> vmcnt(0) -> barrier -> agent release -> ticket
+// fetch_add; the last arriver acquires before reading y2 (MI355X_MICROARCH.md, inter-workgroup
+// visibility), and resets the ticket for the next launch (the fc1 launch also zeroes it first).
+constexpr int kTailMaxLogits = 4096;  // B * N3 staged in LDS for the softmax
+
+template <int BT>
+__global__ __launch_bounds__(64 * kLinWaves) void fc23_kernel(
+    const float *__restrict__ y1, int64_t ld1, int B, int64_t K2, const float *__restrict__ W2,
+    const float *__restrict__ b2, float *__restrict__ y2, int64_t N2, const float *__restrict__ W3,
+    const float *__restrict__ b3, int N3, int flags, float *__restrict__ out, int64_t ldo,
+    int64_t *__restrict__ amax, unsigned *ticket, int vec) {
+    __shared__ float logits[kTailMaxLogits];
+    __shared__ int is_last;
+    linear_rows_block<BT>(y1, ld1, B, K2, W2, b2, y2, N2, N2, 1, vec);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = t == gridDim.x * gridDim.y - 1;
+    }
+    __syncthreads();
+    if (!is_last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const int tot = B * N3;
+    const bool vec3 = vec && (N2 & 3) == 0 && (reinterpret_cast<uintptr_t>(W3) & 15) == 0;
+    for (int e = threadIdx.x; e < tot; e += 64 * kLinWaves) {
+        const int b = e / N3, n = e - b * N3;
+        const float *xr = y2 + (int64_t)b * N2, *wr = W3 + (int64_t)n * N2;
+        float a = 0.f;
+        if (vec3) {
+            for (int64_t k = 0; k < N2; k += 4) {
+                const float4 xv = *reinterpret_cast<const float4 *>(xr + k);
+                const float4 wv = *reinterpret_cast<const float4 *>(wr + k);
+                a = fmaf(wv.x, xv.x, a);
+                a = fmaf(wv.y, xv.y, a);
+                a = fmaf(wv.z, xv.z, a);
+                a = fmaf(wv.w, xv.w, a);
+            }
+        } else {
+            for (int64_t k = 0; k < N2; ++k) a = fmaf(wr[k], xr[k], a);
+        }
+        a += b3 ? b3[n] : 0.f;
+        if (flags & PN2_TAIL_LOGSOFTMAX) logits[e] = a;
+        else out[(int64_t)b * ldo + n] = a;
+    }
+    if (flags & PN2_TAIL_LOGSOFTMAX) {
+        __syncthreads();
+        for (int b = threadIdx.x; b < B; b += 64 * kLinWaves) {
+            const float *v = logits + b * N3;
+            float m = v[0];
+            for (int n = 1; n < N3; ++n) m = fmaxf(m, v[n]);
+            float s = 0.f;
+            for (int n = 0; n < N3; ++n) s += expf(v[n] - m);
+            const float ls = logf(s);
+            float best = 0.f;
+            int bi = 0;
+            for (int n = 0; n < N3; ++n) {
+                const float o = (v[n] - m) - ls;
+                out[(int64_t)b * ldo + n] = o;
+                if (n == 0 || o > best) best = o, bi = n;
+            }
+            if (amax) amax[b] = bi;
+        }
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace pn2
 
 using namespace pn2;
@@ -157,10 +248,58 @@ extern "C" int pn2_linear_rows_f32(const float *x, int64_t ldx, int64_t B, int64
     const dim3 block(64 * kLinWaves);
     if (B <= 8)
         hipLaunchKernelGGL(linear_rows_kernel<8>, grid(lin_rows<8>(), 8), block, 0, st, x, ldx, (int)B, K, W, bias,
-                           out, ldo, N, relu, vec);
+                           out, ldo, N, relu, vec, nullptr);
     else
         hipLaunchKernelGGL(linear_rows_kernel<16>, grid(lin_rows<16>(), 16), block, 0, st, x, ldx, (int)B, K, W, bias,
-                           out, ldo, N, relu, vec);
+                           out, ldo, N, relu, vec, nullptr);
     PN2_LAUNCH_CHECK("linear_rows_kernel");
+    return PN2_OK;
+}
+
+static int64_t tail_ws_floats(int64_t B, int64_t N1, int64_t N2) {
+    return (B * N1 + 3) / 4 * 4 + (B * N2 + 3) / 4 * 4;
+}
+
+extern "C" int64_t pn2_fc_tail_workspace_bytes(int64_t B, int64_t N1, int64_t N2) {
+    if (B < 1 || N1 < 1 || N2 < 1) return -1;
+    return tail_ws_floats(B, N1, N2) * 4 + 16;
+}
+
+extern "C" int pn2_fc_tail_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const float *W1,
+                               const float *b1, int64_t N1, const float *W2, const float *b2, int64_t N2,
+                               const float *W3, const float *b3, int64_t N3, int flags, float *out,
+                               int64_t ldo, int64_t *argmax, void *workspace, int64_t workspace_bytes,
+                               void *stream) {
+    PN2_REQUIRE(x && W1 && W2 && W3 && out && workspace, "pn2_fc_tail_f32: null pointer");
+    PN2_REQUIRE(B >= 1 && (B + 15) / 16 <= 65535 && K >= 1 && N1 >= 1 && N2 >= 1 && N3 >= 1 &&
+                    ldx >= K && ldo >= N3, "pn2_fc_tail_f32: bad shape");
+    PN2_REQUIRE((flags & ~PN2_TAIL_LOGSOFTMAX) == 0, "pn2_fc_tail_f32: unknown flags");
+    PN2_REQUIRE(B * N3 <= kTailMaxLogits, "pn2_fc_tail_f32: B*N3 = %lld exceeds %d", (long long)(B * N3),
+                kTailMaxLogits);
+    PN2_REQUIRE(workspace_bytes >= pn2_fc_tail_workspace_bytes(B, N1, N2) && ((uintptr_t)workspace & 15) == 0,
+                "pn2_fc_tail_f32: workspace too small or not 16-byte aligned");
+    float *y1 = reinterpret_cast<float *>(workspace);
+    float *y2 = y1 + (B * N1 + 3) / 4 * 4;
+    unsigned *ticket = reinterpret_cast<unsigned *>(y1 + tail_ws_floats(B, N1, N2));
+    hipStream_t st = as_stream(stream);
+    const int vec1 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W1)) & 15) == 0 &&
+                     (K & 3) == 0 && (ldx & 3) == 0;
+    const int vec2 = (reinterpret_cast<uintptr_t>(W2) & 15) == 0 && (N1 & 3) == 0;
+    auto grid = [B](int64_t N, int rows, int bt) {
+        return dim3((unsigned)((N + rows - 1) / rows), (unsigned)((B + bt - 1) / bt));
+    };
+    const dim3 block(64 * kLinWaves);
+    if (B <= 8) {
+        hipLaunchKernelGGL(linear_rows_kernel<8>, grid(N1, lin_rows<8>(), 8), block, 0, st, x, ldx, (int)B, K, W1,
+                           b1, y1, N1, N1, 1, vec1, ticket);
+        hipLaunchKernelGGL(fc23_kernel<8>, grid(N2, lin_rows<8>(), 8), block, 0, st, y1, N1, (int)B, N1, W2, b2,
+                           y2, N2, W3, b3, (int)N3, flags, out, ldo, argmax, ticket, vec2);
+    } else {
+        hipLaunchKernelGGL(linear_rows_kernel<16>, grid(N1, lin_rows<16>(), 16), block, 0, st, x, ldx, (int)B, K,
+                           W1, b1, y1, N1, N1, 1, vec1, ticket);
+        hipLaunchKernelGGL(fc23_kernel<16>, grid(N2, lin_rows<16>(), 16), block, 0, st, y1, N1, (int)B, N1, W2, b2,
+                           y2, N2, W3, b3, (int)N3, flags, out, ldo, argmax, ticket, vec2);
+    }
+    PN2_LAUNCH_CHECK("fc23_kernel");
     return PN2_OK;
 }

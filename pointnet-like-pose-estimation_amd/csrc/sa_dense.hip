@@ -28,9 +28,10 @@ namespace pn2 {
 
 // Timeline stamps (diagnostic builds only: -DPN2_DENSE_STAMPS, tools/debug/dense_stamps.py):
 // s_memrealtime (100 MHz, chip-wide) of every workgroup of the last launch, wave 0 lane 0:
-// [0] entry, [1 + c] past stage c's barrier (c < 12), [14] main loop done, [15] exit.
+// [0] entry, [1 + c] past stage c's barrier (c < 12), [14] main loop done, [15] exit; [16] /
+// [17] s_memtime (shader clock) at entry / exit.
 #ifdef PN2_DENSE_STAMPS
-constexpr int kDStampWG = 4096, kDStamps = 16;
+constexpr int kDStampWG = 4096, kDStamps = 18;
 __device__ unsigned long long g_dense_stamps[kDStampWG * kDStamps];
 #define PN2_DSTAMP(i)                                                                           \
     do {                                                                                        \
@@ -42,8 +43,15 @@ extern "C" int pn2_debug_dense_stamps(unsigned long long *dst, int64_t n) {
     const int64_t m = n < (int64_t)kDStampWG * kDStamps ? n : (int64_t)kDStampWG * kDStamps;
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dense_stamps), m * 8) == hipSuccess ? 0 : -1;
 }
+#define PN2_DCLOCK(i)                                                                           \
+    do {                                                                                        \
+        const unsigned b_ = blockIdx.x + blockIdx.y * gridDim.x;                                \
+        if (threadIdx.x == 0 && b_ < kDStampWG)                                                 \
+            g_dense_stamps[b_ * kDStamps + (i)] = __builtin_amdgcn_s_memtime();                 \
+    } while (0)
 #else
 #define PN2_DSTAMP(i) do {} while (0)
+#define PN2_DCLOCK(i) do {} while (0)
 #endif
 
 constexpr int kDW = 4;            // waves per workgroup
@@ -76,6 +84,9 @@ struct DenseSplitArgs {
     // atomicMax pool, so that layer needs no memset launch of its own
     float *zero;
     int64_t zrows, zcols, zstride;
+    // dense_lds_kernel: XCD x runs a (row blocks / (8 / xcx)) x (column tiles / xcx) rectangle of
+    // the output (0: XCD-contiguous logical ids, whole row blocks per XCD)
+    int xcx;
 };
 
 // Signed max through unsigned atomics: key() is monotone from float order to uint order (and
@@ -99,6 +110,13 @@ __global__ void unkey_kernel(float *out, int64_t ostride, int64_t G, int cols) {
 // one lane-linear 16-byte-per-lane copy HBM/L2 -> LDS (global_load_lds, no VGPR destination)
 __device__ __forceinline__ void dma16(const char *src, char *dst) {
     __builtin_amdgcn_global_load_lds(src, (lds_void *)dst, 16, 0, 0);
+}
+
+// raw s_barrier (__syncthreads' fence would wait vmcnt(0) and drain the DMA ring)
+__device__ __forceinline__ void stage_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 }
 
 template <int NTC, int NP, bool FAST, int NW>
@@ -420,6 +438,393 @@ static int launch_dense_split(const DenseSplitArgs &A, hipStream_t st) {
     return PN2_OK;
 }
 
+// ------------------------------------------------------------------ LDS-staged dense layer
+// The same layer with BOTH operands staged in LDS by global_load_lds: the A rows as whole
+// 128-byte lines (32 fp32 channels per row and stage) instead of two 16-byte pieces per lane
+// from 32 different rows (the pattern that bounded dense_split_kernel's stages: its load stage
+// alone took 1.7 of its ~2.5 us, tools/micro/row_loads.hip), and the B fragments as before.
+// Tiles are TR x TC = 32*WR x 32*NTW with WR waves; wave w computes rows 32w.. x every column
+// of the tile (NTW 32-column MFMA tiles), so each A element is split into its bf16 planes once
+// per workgroup -- the split is the VALU cost that competes with the MFMAs for issue slots.
+// An NS-stage ring (stage = 32 input channels) keeps NS-2 stages' DMA in flight: a counted
+// vmcnt and a raw s_barrier per stage, never vmcnt(0) inside the loop.
+//
+// A's LDS image is [TR rows][8 chunks of 16 B]; chunk c of row r is stored at c ^ ((r>>1) & 7)
+// (DMA writes lane-linearly, so the swizzle is on the source address): the two ds_read_b128 of
+// an A fragment (chunks 4kb+h and 4kb+2+h of 32 consecutive rows) then cover all 64 banks in
+// every 16-lane group of the b128 read (conflict-free for gfx950's lane grouping; SQ counters:
+// no bank conflicts).
+//
+// Sources: rows mode (dense fp32 rows, row stride rs, cin % 32 == 0, 16-byte aligned) and
+// group_all (block 0 = xyz of the point, read straight into registers before the loop; then
+// the features, D % 32 == 0).  Epilogue as dense_split_kernel (raw / BN + ReLU / no-ReLU, and
+// pools over K rows when K % 32 == 0 and K divides TR or TR divides K).  Every product and
+// accumulation is the one dense_split_kernel computes, in the same k order: the same bits.
+// (LDS keeps one workgroup of 8 waves, or 2-4 waves, per CU: the register file allows up to 256
+// VGPRs per wave, and the scheduler may use them to issue a stage's fragment reads early)
+template <int WR, int NTW, int NP, int NS>
+__global__ __launch_bounds__(64 * WR) __attribute__((amdgpu_waves_per_eu(WR == 8 ? 2 : 1, WR == 8 ? 2 : 1)))
+void dense_lds_kernel(const DenseSplitArgs A) {
+    constexpr int NW = WR;
+    constexpr int TR = 32 * WR, TC = 32 * NTW, NT = NTW;
+    constexpr int kAStage = TR * 128;             // TR rows x 32 channels x 4 B
+    constexpr int kBStage = 2 * NT * NP * 1024;   // 2 k-blocks x NT tiles x NP planes
+    constexpr int kStage = kAStage + kBStage;
+    constexpr int kAIns = kAStage / 1024, kIns = kAIns + kBStage / 1024;  // DMA per stage
+    constexpr int kMaxPer = (kIns + NW - 1) / NW;
+    extern __shared__ __attribute__((aligned(16))) char lsm[];
+    PN2_DSTAMP(0);
+    PN2_DCLOCK(16);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // this wave's DMA instructions per stage: i = wave + NW j < kIns (the first kIns % NW
+    // waves issue one more)
+    const bool more = kIns % NW != 0 && wave < kIns % NW;
+    const unsigned ntile = (unsigned)(A.tiles / NT);
+    unsigned rbi, cti;  // row block, column tile
+    if (A.xcx > 0) {
+        // dispatch deals workgroup i to XCD i % 8: XCD x gets a rectangle of row blocks x column
+        // tiles, so its L2 holds a share of both operands
+        const unsigned x = blockIdx.x & 7u, i = blockIdx.x >> 3;
+        const unsigned cx = (unsigned)A.xcx, nr = gridDim.x / ntile;
+        const unsigned rpx = nr / (8u / cx), cpx = ntile / cx;
+        rbi = (x / cx) * rpx + i / cpx;
+        cti = (x % cx) * cpx + i % cpx;
+    } else {
+        const unsigned lid = xcd_contiguous(blockIdx.x, gridDim.x);
+        rbi = lid / ntile;
+        cti = lid % ntile;
+    }
+    const int row0 = (int)rbi * TR;
+    const int ct0 = (int)cti * NT;  // first 32-column tile of the workgroup
+    if (A.zero) {  // a side job: the next layer's pool, or the caller's zero_out
+        const int64_t tot = A.zrows * A.zcols, nwg = gridDim.x;
+        const int64_t per = (tot + nwg - 1) / nwg, e0 = (int64_t)blockIdx.x * per;
+        const int64_t e1 = e0 + per < tot ? e0 + per : tot;
+        for (int64_t e = e0 + tid; e < e1; e += 64 * NW) {
+            const int64_t g = e / A.zcols;
+            A.zero[g * A.zstride + (e - g * A.zcols)] = 0.f;
+        }
+    }
+    const int kb0 = A.mode == 1 ? 1 : 0;        // group_all: block 0 = xyz (registers)
+    const int nst = (A.kb - kb0) / 2;           // 32-channel stages
+
+    // ---- this lane's DMA sources.  A instruction i < kAIns covers tile rows 8i .. 8i+7: lane l
+    // -> row + (l >> 3), LDS chunk l & 7, source chunk (l & 7) ^ ((row >> 1) & 7).  B
+    // instruction i >= kAIns is fragment f = i - kAIns = (kbl * NT + t) * NP + p of the stage.
+    const int64_t plane = (int64_t)A.tiles * A.kb * 64;
+    const unsigned loff = (unsigned)lane * 16u;
+    const char *src[kMaxPer];
+    int64_t step[kMaxPer];  // source bytes per stage
+#pragma unroll
+    for (int j = 0; j < kMaxPer; ++j) {
+        const int i = min(wave + NW * j, kIns - 1);
+        if (i < kAIns) {
+            const int tr = 8 * i + (lane >> 3);
+            const int R = min(row0 + tr, A.M - 1);  // rows past M: any valid row, never stored
+            const int chunk = (lane & 7) ^ ((tr >> 1) & 7);
+            const float *base;
+            if (A.mode == 0) {
+                base = A.rows + (int64_t)R * A.rs;
+            } else {
+                const int b = R / A.N, n = R - b * A.N;
+                base = A.feat + (int64_t)b * A.fb + (int64_t)n * A.fn;
+            }
+            src[j] = reinterpret_cast<const char *>(base + 4 * chunk);
+            step[j] = 32 * 4;
+        } else {
+            const int f = i - kAIns;
+            const int p = f % NP, t = (f / NP) % NT, kbl = f / (NP * NT);
+            src[j] = reinterpret_cast<const char *>(A.w + p * plane + ((int64_t)(ct0 + t) * A.kb + kb0 + kbl) * 64) + loff;
+            step[j] = 2 * 1024;
+        }
+    }
+    auto issue = [&](int st) {
+        char *buf = lsm + (st % NS) * kStage;
+#pragma unroll
+        for (int j = 0; j < kMaxPer; ++j) {
+            const int i = wave + NW * j;
+            if (j < kMaxPer - 1 || kIns % NW == 0 || more)
+                dma16(src[j] + st * step[j], buf + i * 1024);
+        }
+    };
+
+    cfloatx16 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][q] = 0.f;
+
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < nst) issue(s);
+    const int trow = 32 * wave + r;  // this lane's tile row (A fragment)
+    if (A.mode == 1) {
+        // block 0: raw xyz of the point (sample_and_group_all does not centre), and its
+        // fragments straight from L2
+        const int R = min(row0 + trow, A.M - 1);
+        const int b = R / A.N, n = R - b * A.N;
+        const float *prow = A.pts + (int64_t)b * A.pb + (int64_t)n * A.pn;
+        float x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int ch = (j & 3) + 8 * (j >> 2) + 4 * h;
+            x[j] = ch < A.C ? prow[(int64_t)ch * A.pc] : 0.f;
+        }
+        const Split xs = splitN<NP>(x);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            const bf16x8 *wq = A.w + (int64_t)(ct0 + i) * A.kb * 64 + lane;
+            Split w;
+            w.h = wq[0];
+            w.m = NP == 3 ? wq[plane] : w.h;
+            w.l = NP == 3 ? wq[2 * plane] : w.h;
+            acc[i] = mma_wb<NP>(xs, w, acc[i]);
+        }
+    }
+    const int swz = (trow >> 1) & 7;
+    constexpr int kLo = kIns / NW, kHi = kLo + (kIns % NW ? 1 : 0);
+    // the epilogue's BN scale / shift, loaded now (their latency hides under the main loop)
+    float eal[NT], ebe[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        const int col = 32 * (ct0 + i) + r;
+        eal[i] = A.raw ? 1.f : A.alpha[col];
+        ebe[i] = A.raw ? 0.f : A.beta[col];
+    }
+    // ---- main loop, software-pipelined across stages.  Without it both waves of a SIMD left
+    // each barrier together and split their A fragments together, with the matrix pipe idle
+    // (the stage's arithmetic alone ran at ~55 % of its MFMA time, tools/debug/dense_stamps.py
+    // on a no-DMA build).  Now stage st's k-block 0 MFMAs are issued first; behind them the
+    // wave passes the barrier of stage st+1, issues its reads and splits its A fragments
+    // under stage st's k-block 1 MFMAs.  Stage st+NS overwrites stage st's buffer: every wave's
+    // reads of it returned before it reached the barrier of stage st+1.
+    // this wave's DMA of stage s has landed, `y` younger stages may stay in flight
+    auto wait_dma = [&](int y) {
+        if (y >= 2) {
+            if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kHi) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kLo) : "memory");
+        } else if (y == 1) {
+            if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kHi) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLo) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    };
+    struct Frags {
+        cfloatx4 a[2][2];
+        Split b[2][NT];
+    };
+    // the stage's fragments, all reads issued together (A first: its split is the first use)
+    auto read_stage = [&](int st, Frags &f) {
+        const char *buf = lsm + (st % NS) * kStage;
+        const char *arow = buf + trow * 128;
+#pragma unroll
+        for (int kbl = 0; kbl < 2; ++kbl) {
+            f.a[kbl][0] = *reinterpret_cast<const cfloatx4 *>(arow + (((4 * kbl + h) ^ swz) << 4));
+            f.a[kbl][1] = *reinterpret_cast<const cfloatx4 *>(arow + (((4 * kbl + 2 + h) ^ swz) << 4));
+        }
+#pragma unroll
+        for (int kbl = 0; kbl < 2; ++kbl)
+#pragma unroll
+            for (int i = 0; i < NT; ++i) f.b[kbl][i] = ring_readN<NP>(buf + kAStage + ((kbl * NT + i) * NP) * 1024, lane);
+    };
+    auto split_stage = [&](const Frags &f, Split (&xs)[2]) {
+#pragma unroll
+        for (int kbl = 0; kbl < 2; ++kbl) {
+            float x[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = f.a[kbl][0][i], x[4 + i] = f.a[kbl][1][i];
+            xs[kbl] = splitN<NP>(x);
+        }
+    };
+    auto mfma_kb = [&](const Split &xs, const Frags &f, int kbl) {
+#ifdef PN2_DENSE_DIAG_NOMFMA  // diagnostic builds only (wrong results): no MFMAs in the loop
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            asm volatile("" ::"v"(xs.h), "v"(xs.m), "v"(xs.l), "v"(f.b[kbl][i].h), "v"(f.b[kbl][i].m), "v"(f.b[kbl][i].l));
+            acc[i][0] += 1.f;
+        }
+#else
+#pragma unroll
+        for (int i = 0; i < NT; ++i) acc[i] = mma_wb<NP>(xs, f.b[kbl][i], acc[i]);
+#endif
+    };
+    // barrier of stage s (its DMA landed everywhere, stage s-1's buffer is free) + the DMA of
+    // stage s+NS-1 into it
+    auto enter_stage = [&](int s) {
+        wait_dma(min(NS - 2, nst - 1 - s));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stage_barrier();
+        if (s < 12) PN2_DSTAMP(1 + s);
+#ifndef PN2_DENSE_DIAG_NODMA  // diagnostic builds only (wrong results): no loads in the loop
+        if (s + NS - 1 < nst) issue(s + NS - 1);
+#endif
+    };
+    // one stage with the next one's entry, reads and split behind its MFMAs
+    auto stage_step = [&](int st, const Frags &cur, const Split (&xc)[2], Frags &nxt, Split (&xn)[2]) {
+        mfma_kb(xc[0], cur, 0);
+        enter_stage(st + 1);
+        read_stage(st + 1, nxt);
+        mfma_kb(xc[1], cur, 1);
+        split_stage(nxt, xn);
+    };
+    if (nst > 0) {
+        Frags fa, fb;
+        Split xa[2], xb[2];
+        enter_stage(0);
+        read_stage(0, fa);
+        split_stage(fa, xa);
+        int st = 0;
+        for (; st + 2 < nst; st += 2) {
+            stage_step(st, fa, xa, fb, xb);
+            stage_step(st + 1, fb, xb, fa, xa);
+        }
+        if (st + 1 < nst) {
+            stage_step(st, fa, xa, fb, xb);
+            mfma_kb(xb[0], fb, 0);
+            mfma_kb(xb[1], fb, 1);
+        } else {
+            mfma_kb(xa[0], fa, 0);
+            mfma_kb(xa[1], fa, 1);
+        }
+    }
+    __syncthreads();  // the stage buffers are free again (the pool below reuses them)
+    PN2_DSTAMP(14);
+
+    // ---- epilogue: lane = output column, register q = row (q&3) + 8(q>>2) + 4h of the slab
+    const int slab_row = row0 + 32 * wave;
+    const unsigned G = A.pool ? (unsigned)A.M / (unsigned)A.K : 0u;
+    const bool lds_pool = A.pool && TR % A.K == 0;
+    const int gpb = lds_pool ? TR / A.K : 0;
+    unsigned *opool = reinterpret_cast<unsigned *>(lsm);  // [gpb][TC]
+    if (lds_pool) {
+        for (int e = tid; e < gpb * TC; e += 64 * NW) opool[e] = 0u;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        const int lcol = 32 * i + r;
+        const int col = 32 * ct0 + lcol;
+        const float al = eal[i], be = ebe[i];
+        if (!A.pool) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = slab_row + (q & 3) + 8 * (q >> 2) + 4 * h;
+                if (row < A.M) {
+                    const float y = __builtin_fmaf(acc[i][q], al, be);
+                    A.out[(int64_t)row * A.ostride + col] = A.raw ? acc[i][q] : (A.norelu ? y : chain_relu(y));
+                }
+            }
+            continue;
+        }
+        // max over rows of relu(fma(acc, al, be)) = relu(fma(row max (al >= 0) or min, al, be))
+        float mx = acc[i][0], mn = acc[i][0];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) {
+            mx = fmaxf(mx, acc[i][q]);
+            mn = fminf(mn, acc[i][q]);
+        }
+        mx = fmaxf(mx, swap_halves(mx));
+        mn = fminf(mn, swap_halves(mn));
+        const float y = __builtin_fmaf(al >= 0.f ? mx : mn, al, be);
+        const float m = A.norelu ? y : chain_relu(y);
+        // ReLU output >= +0: its bits order as uints; signed (norelu) values go through fkey
+        const unsigned mk = A.norelu ? fkey(m) : __float_as_uint(m);
+        if (h == 0 && slab_row < A.M) {
+            const unsigned gg = (unsigned)slab_row / (unsigned)A.K;
+            if (lds_pool)
+                atomicMax(opool + ((int)gg - row0 / A.K) * TC + lcol, mk);
+            else
+                atomicMax(reinterpret_cast<unsigned *>(A.out + (int64_t)gg * A.ostride + col), mk);
+        }
+    }
+    if (lds_pool) {
+        __syncthreads();
+        for (int e = tid; e < gpb * TC; e += 64 * NW) {
+            const int gl = e / TC, c = e - gl * TC;
+            const unsigned gg = (unsigned)(row0 / A.K + gl);
+            if (gg < G)
+                A.out[(int64_t)gg * A.ostride + 32 * ct0 + c] =
+                    A.norelu ? funkey(opool[e]) : __uint_as_float(opool[e]);
+        }
+    }
+    PN2_DSTAMP(15);
+    PN2_DCLOCK(17);
+}
+
+// Tiles of the LDS-staged kernel, as WR * 10 + NTW (rows 32 WR, columns 32 NTW): the first that
+// leaves a workgroup per CU -- 256 x 64 (8 waves, 2 per SIMD), 128 x 128 (4 waves), 128 x 64,
+// 64 x 64 -- and pools (0: not eligible).  Tuning dense_lds_tile forces one.
+static const int kLdsTiles[] = {82, 44, 42, 22};
+
+static int dense_lds_tile(const DenseSplitArgs &A) {
+    if (!tuning().dense_lds || !A.vec) return 0;
+    const bool ok = A.mode == 0 ? (A.cin % 32 == 0 && A.kb * 16 == A.cin && A.rs % 4 == 0 &&
+                                   ((uintptr_t)A.rows & 15) == 0)
+                                : (A.feat && A.D > 0 && A.D % 32 == 0 && A.kb == 1 + A.D / 16 &&
+                                   A.fn % 4 == 0 && A.fb % 4 == 0 && ((uintptr_t)A.feat & 15) == 0);
+    if (!ok) return 0;
+    auto fits = [&](int t) {
+        const int tr = 32 * (t / 10), ntw = t % 10;
+        return A.tiles % ntw == 0 && (!A.pool || (A.K % 32 == 0 && (tr % A.K == 0 || A.K % tr == 0)));
+    };
+    if (const int64_t f = tuning().dense_lds_tile) return fits((int)f) ? (int)f : 0;
+    for (int t : kLdsTiles) {
+        const int tr = 32 * (t / 10), ntw = t % 10;
+        if (fits(t) && (A.M + tr - 1) / tr * (A.tiles / ntw) >= 256) return t;
+    }
+    return fits(22) ? 22 : 0;
+}
+
+template <int WR, int NTW, int NP, int NS>
+static int launch_dense_lds_ns(DenseSplitArgs A, hipStream_t st) {
+    constexpr int TR = 32 * WR, NT = NTW;
+    const size_t stage = (size_t)TR * 128 + (size_t)2 * NT * NP * 1024;
+    const size_t pool = A.pool && TR % A.K == 0 ? (size_t)(TR / A.K) * 32 * NT * 4 : 0;
+    const size_t lds = std::max((size_t)NS * stage, pool);
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void *>(&dense_lds_kernel<WR, NTW, NP, NS>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)attr;
+    const int64_t nr = (A.M + TR - 1) / TR, nc = A.tiles / NT;
+    // XCD rectangles: the column split cx (1, 2, 4, 8) that holds the fewest operand bytes per
+    // XCD, when the grid divides evenly (tuning dense_lds_xcd2d = 0: whole row blocks per XCD)
+    A.xcx = 0;
+    if (tuning().dense_lds_xcd2d && (nr * nc) % 8 == 0) {
+        const int64_t abytes = (int64_t)TR * A.kb * 64, bbytes = (int64_t)32 * NT * A.kb * 16 * 2 * NP;
+        int64_t best = -1;
+        for (int cx = 1; cx <= 8; cx *= 2) {
+            if (nc % cx || nr % (8 / cx)) continue;
+            const int64_t b = nr / (8 / cx) * abytes + nc / cx * bbytes;
+            if (best < 0 || b < best) best = b, A.xcx = cx;
+        }
+    }
+    hipLaunchKernelGGL((dense_lds_kernel<WR, NTW, NP, NS>), dim3((unsigned)(nr * nc)), dim3(64 * WR), lds, st, A);
+    PN2_LAUNCH_CHECK("dense_lds_kernel");
+    return PN2_OK;
+}
+
+// ring depth: tuning dense_lds_stages (3 or 4; 4 only where four stages fit the CU's LDS)
+template <int WR, int NTW, int NP>
+static int launch_dense_lds(const DenseSplitArgs &A, hipStream_t st) {
+    constexpr size_t stage = (size_t)32 * WR * 128 + (size_t)2 * NTW * NP * 1024;
+    if constexpr (4 * stage <= 160 * 1024)
+        if (tuning().dense_lds_stages >= 4) return launch_dense_lds_ns<WR, NTW, NP, 4>(A, st);
+    return launch_dense_lds_ns<WR, NTW, NP, 3>(A, st);
+}
+
+static int launch_dense_lds_tile(int tile, const DenseSplitArgs &A, int np, hipStream_t st) {
+    switch (tile) {
+        case 82: return np == 3 ? launch_dense_lds<8, 2, 3>(A, st) : launch_dense_lds<8, 2, 1>(A, st);
+        case 44: return np == 3 ? launch_dense_lds<4, 4, 3>(A, st) : launch_dense_lds<4, 4, 1>(A, st);
+        case 42: return np == 3 ? launch_dense_lds<4, 2, 3>(A, st) : launch_dense_lds<4, 2, 1>(A, st);
+        default: return np == 3 ? launch_dense_lds<2, 2, 3>(A, st) : launch_dense_lds<2, 2, 1>(A, st);
+    }
+}
+
 // Large layers take 256 x 128 tiles (see dense_split_layer); the rows a launch's workgroup
 // covers decide which pools fit in LDS
 static bool dense_wide(const DenseSplitArgs &A) {
@@ -433,7 +838,32 @@ static int dense_pool_mode(const DenseSplitArgs &A) {
     return 2;
 }
 
+// whether the layer, as it will be launched, pools through HBM atomics into a zeroed output
+static bool dense_needs_zero(const DenseSplitArgs &A) {
+    if (!A.pool) return false;
+    const int tile = dense_lds_tile(A);
+    if (tile) return (32 * (tile / 10)) % A.K != 0;
+    return dense_pool_mode(A) == 2;
+}
+
 static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st, bool prezeroed = false) {
+    if (const int tile = dense_lds_tile(A)) {
+        const bool hbm = dense_needs_zero(A);
+        const int64_t G = A.pool ? A.M / A.K : 0, cols = 32 * (int64_t)A.tiles;
+        if (hbm && !prezeroed) {
+            hipError_t e = A.ostride == cols
+                               ? hipMemsetAsync(A.out, 0, (size_t)G * cols * 4, st)
+                               : hipMemset2DAsync(A.out, (size_t)A.ostride * 4, 0, (size_t)cols * 4, (size_t)G, st);
+            if (e != hipSuccess) return set_error(PN2_EHIP, "dense_lds: memset: %s", hipGetErrorString(e));
+        }
+        const int rc = launch_dense_lds_tile(tile, A, np, st);
+        if (rc == PN2_OK && hbm && A.norelu) {  // keys -> floats
+            hipLaunchKernelGGL(unkey_kernel, dim3((unsigned)((G * cols + 255) / 256)), dim3(256), 0, st,
+                               A.out, A.ostride, G, (int)cols);
+            PN2_LAUNCH_CHECK("unkey_kernel");
+        }
+        return rc;
+    }
     // Large layers (e.g. translation_ssg's group_all over B*512 rows) take 256 x 128 tiles (8
     // waves of 32 rows x 4 column tiles): the 128 x 64 tile re-reads its A rows once per 64
     // output columns and its weights once per 128 rows, and at these sizes that L2 -> CU
@@ -557,7 +987,13 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
     // a last layer that pools by HBM atomics gets its output zeroed by the layer before it
     // (one launch fewer than a memset: PointNet-v1's max over N points, group_all over K > 256)
     DenseSplitArgs last = make(nlayers - 1);
-    const bool fold_zero = nlayers > 1 && last.pool && dense_pool_mode(last) == 2;
+    const bool fold_zero = nlayers > 1 && last.pool && dense_needs_zero(last);
+    if (s.zero_out && s.zero_count > 0) {  // the caller's side job rides on the last layer
+        last.zero = s.zero_out;
+        last.zrows = 1;
+        last.zcols = s.zero_count;
+        last.zstride = s.zero_count;
+    }
     for (int l = 0; l < nlayers; ++l) {
         DenseSplitArgs A = l == nlayers - 1 ? last : make(l);
         if (fold_zero && l == nlayers - 2) {

@@ -868,6 +868,14 @@ static int run_plan(const pn2_sa_src &cur, const pn2_mlp_layer *layers, int l0, 
 static thread_local int g_last_path = 0;
 extern "C" int pn2_sa_mlp_last_path(void) { return g_last_path; }
 
+// the src's zero side job on the paths whose kernels do not take it (the dense-layer path's
+// last layer does)
+static int zero_side_job(const pn2_sa_src &s, hipStream_t st) {
+    if (!s.zero_out || s.zero_count <= 0) return PN2_OK;
+    const hipError_t e = hipMemsetAsync(s.zero_out, 0, (size_t)s.zero_count * 4, st);
+    return e == hipSuccess ? PN2_OK : set_error(PN2_EHIP, "pn2_sa_mlp_max: zero_out: %s", hipGetErrorString(e));
+}
+
 extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers,
                                   int nlayers, int pool, float *out, int64_t ostride,
                                   float *workspace, int64_t workspace_bytes, void *stream) {
@@ -883,7 +891,7 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
                           workspace_bytes, st);
     if (rc != 0) {
         if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
-        return rc < 0 ? rc : PN2_OK;
+        return rc < 0 ? rc : zero_side_job(*src, st);
     }
     rc = try_launch_dense_split(*src, layers, nlayers, pool, out, ostride, workspace, workspace_bytes,
                                 M, K, 3, st);
@@ -891,6 +899,7 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
         if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
         return rc < 0 ? rc : PN2_OK;
     }
+    if ((rc = zero_side_job(*src, st)) != PN2_OK) return rc;
     for (int l = 0; l < nlayers; ++l)
         if (layers[l].flags & PN2_LAYER_NO_RELU)
             return set_error(PN2_EUNSUPPORTED, "pn2_sa_mlp_max_f32: layer %d without ReLU needs the split "
@@ -954,6 +963,7 @@ extern "C" int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *l
     hipStream_t st = as_stream(stream);
     rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, 1, workspace,
                           workspace_bytes, st);
+    if (rc > 0 && (rc = zero_side_job(*src, st)) == PN2_OK) rc = 1;
     if (rc == 0)
         rc = try_launch_dense_split(*src, layers, nlayers, pool, out, ostride, workspace,
                                     workspace_bytes, M, K, 1, st);

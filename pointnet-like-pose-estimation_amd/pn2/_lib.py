@@ -43,6 +43,7 @@ class SaSrc(ctypes.Structure):
         ("rows", _vp), ("rs", _i64),
         ("B", _i64), ("N", _i64), ("C", _i64), ("D", _i64), ("S", _i64), ("K", _i64),
         ("cnt", _vp),
+        ("zero_out", _vp), ("zero_count", _i64),
     ]
 
 
@@ -55,6 +56,7 @@ PATH_SPLIT_BF16 = 2
 PATH_BF16 = 3
 LAYER_NO_RELU = 1
 LINEAR_RELU = 1
+TAIL_LOGSOFTMAX = 1
 DEVERR_NO_NEIGHBOUR = 1
 DEVERR_INDEX = 2
 
@@ -104,6 +106,9 @@ SIGNATURES = {
     "pn2_tuning_set": (_int, [ctypes.c_char_p, _i64]),
     "pn2_tuning_keys": (ctypes.c_char_p, []),
     "pn2_device_errors": (_int, [_int, ctypes.POINTER(ctypes.c_uint32)]),
+    "pn2_fc_tail_workspace_bytes": (_i64, [_i64, _i64, _i64]),
+    "pn2_fc_tail_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64,
+                               _int, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
 
 ABI_VERSION = 10

@@ -25,23 +25,49 @@ import torch.nn.functional as F
 from .pointnet2_utils import PointNetSetAbstraction as SA
 from .pointnet2_utils import PointNetSetAbstractionMsg as SAMsg
 from .pointnet2_utils import _needs_autograd
-from .pointnet_utils import linear_bn
+from . import ops
+from .pointnet_utils import _fold_linear, linear_bn
 
 
 class _FCHead(nn.Module):
     """fc1/bn1/relu/drop -> fc2/bn2/relu/drop -> fc3, shared by every head.  Eval without
-    autograd: each fc + bn folded into one GEMM with the ReLU, and fc3, on pn2's row kernel
-    (pn2.pointnet_utils.linear_bn; dropout is the identity in eval)."""
+    autograd: each fc + bn folded into one (W', b') and the whole tail in two launches
+    (pn2.ops.fc_tail: fc1 over the grid, then fc2 over the grid and fc3 -- with the
+    classifiers' log_softmax and argmax -- in its last workgroup; dropout is the identity in
+    eval).  Otherwise, or when a layer cannot fold, the reference's modules."""
+
+    def _folded(self):
+        c = self._fc_cache
+        wb = [_fold_linear(self.fc1, self.bn1, c.setdefault(1, {})),
+              _fold_linear(self.fc2, self.bn2, c.setdefault(2, {})),
+              _fold_linear(self.fc3, None, c.setdefault(3, {}))]
+        return None if any(t is None for t in wb) else wb
+
+    def _fused_ok(self, x):
+        return (not _needs_autograd(self, x) and x.is_cuda and x.dtype == torch.float32 and
+                x.dim() == 2 and x.stride(1) == 1 and x.shape[0] * self.fc3.out_features <= 4096)
 
     def _fc(self, x):
+        if self._fused_ok(x):
+            wb = self._folded()
+            if wb is not None:
+                return ops.fc_tail(x, wb, False)[0]
         if not _needs_autograd(self, x):
             x = linear_bn(x, self.fc1, self.bn1, self._fc_cache.setdefault(1, {}))
             x = linear_bn(x, self.fc2, self.bn2, self._fc_cache.setdefault(2, {}))
-            # fc3 on the same row kernel (a library GEMM launch for 256 -> 3 / 7 took ~5 us)
             return linear_bn(x, self.fc3, None, self._fc_cache.setdefault(3, {}), relu=False)
         x = self.drop(F.relu(self.bn1(self.fc1(x))))
         x = self.drop(F.relu(self.bn2(self.fc2(x))))
         return self.fc3(x)
+
+    def _fc_log_softmax(self, x):
+        """(F.log_softmax(fc(x), -1), its first argmax per row): pointnet2_cls_ssg.py:36-38."""
+        if self._fused_ok(x):
+            wb = self._folded()
+            if wb is not None:
+                return ops.fc_tail(x, wb, True)
+        y = F.log_softmax(self._fc(x), -1)
+        return y, y.data.max(1)[1]
 
     def _make_fc(self, out):
         self.fc1 = nn.Linear(1024, 512)
@@ -66,8 +92,8 @@ class ClsSSG(_FCHead):
         l1p, l1f = self.sa1(points, None)
         l2p, l2f = self.sa2(l1p, l1f)
         _, l3f = self.sa3(l2p, l2f)
-        x = F.log_softmax(self._fc(l3f.reshape(B, 1024)), -1)
-        return x, l3f, x.data.max(1)[1]
+        x, pred = self._fc_log_softmax(l3f.reshape(B, 1024))
+        return x, l3f, pred
 
 
 class ClsMSG(_FCHead):
@@ -83,8 +109,8 @@ class ClsMSG(_FCHead):
         l1p, l1f = self.sa1(points, None)
         l2p, l2f = self.sa2(l1p, l1f)
         _, l3f = self.sa3(l2p, l2f)
-        x = F.log_softmax(self._fc(l3f.reshape(B, 1024)), -1)
-        return x, l3f, x.data.max(1)[1]
+        x, pred = self._fc_log_softmax(l3f.reshape(B, 1024))
+        return x, l3f, pred
 
 
 class RotationSSG(_FCHead):

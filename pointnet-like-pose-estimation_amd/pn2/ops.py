@@ -377,7 +377,7 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
                 alphas: List[Tensor], betas: List[Tensor], cins: List[int],
                 splits: List[Tensor], precision: str = "fp32", flags: Optional[List[int]] = None,
                 rows: Optional[Tensor] = None, pool: bool = True,
-                cnt: Optional[Tensor] = None) -> None:
+                cnt: Optional[Tensor] = None, zero: Optional[Tensor] = None) -> None:
     """Fused gather -> MLP (conv1x1+BN+ReLU)* -> max over each group, written channels-last
     into `out` ([G, >=cout] view with unit column stride; G = B*S groups, or B for
     group_all).  mode: 0 SSG grouping, 1 MSG grouping, 2 group_all, 3 rows (`rows` [B, R, cin]
@@ -387,7 +387,8 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
     flags: per-layer PN2_LAYER_* bits (LAYER_NO_RELU).  pool=False: `out` gets every row's
     last-layer output ([M, >=cout], group_all / rows sources).  cnt: the ball query's
     distinct-neighbour counts ([B, S] int32, grouping modes) -- only those rows of each group are
-    computed (the rest repeat the first neighbour; same result)."""
+    computed (the rest repeat the first neighbour; same result).  zero: a contiguous float32
+    tensor one of the call's launches fills with zeros (group_all's new_points)."""
     if precision not in PRECISIONS:
         raise ValueError("pn2::sa_mlp_max_: precision must be one of %s" % (PRECISIONS,))
     bf16 = precision == "bf16"
@@ -416,6 +417,10 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
         src = _src(mode, points, feature, centers, idx, None, B, N, C, D, S, K,
                    cnt if mode in (_lib.SRC_GROUP_XYZ_FIRST, _lib.SRC_GROUP_FEAT_FIRST) else None)
         dev_t = points
+    if zero is not None:
+        if zero.dtype != torch.float32 or not zero.is_contiguous() or zero.device != dev_t.device:
+            raise ValueError("pn2::sa_mlp_max_: zero must be a contiguous float32 device tensor")
+        src.zero_out, src.zero_count = zero.data_ptr(), zero.numel()
     n = len(wts)
     layers = (MlpLayer * n)()
     for i in range(n):
@@ -441,12 +446,12 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
           0 if ws is None else ws.data_ptr(), ws_bytes, _stream(dev_t)), dev_t.device, flops=flops)
 
 
-sa_mlp_max_ = torch.library.custom_op("pn2::sa_mlp_max_", sa_mlp_max_direct, mutates_args=("out",))
+sa_mlp_max_ = torch.library.custom_op("pn2::sa_mlp_max_", sa_mlp_max_direct, mutates_args=("out", "zero"))
 
 
 @sa_mlp_max_.register_fake
 def _(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits, precision="fp32",
-      flags=None, rows=None, pool=True, cnt=None):
+      flags=None, rows=None, pool=True, cnt=None, zero=None):
     return None
 
 
@@ -467,3 +472,30 @@ def linear_rows(x: Tensor, weight: Tensor, bias: Optional[Tensor], relu: bool) -
                                  _lib.LINEAR_RELU if relu else 0, _stream(x)),
           "pn2_linear_rows_f32")
     return out
+
+
+def fc_tail(x: Tensor, layers, logsoftmax: bool):
+    """The heads' eval FC tail on pn2_fc_tail_f32 (two launches): x [B, K] (unit column stride),
+    layers = ((W1, b1), (W2, b2), (W3, b3)) folded float32 (bn1 / bn2 in W1 / W2), fc1 and fc2
+    with ReLU -> (out [B, N3], argmax [B] int64 or None).  logsoftmax: out is
+    log_softmax(fc3(...), -1) and argmax its first per-row maximum (the classifiers' tail,
+    pointnet2_cls_ssg.py:36-38)."""
+    _dev(x, "pn2::fc_tail")
+    (w1, b1), (w2, b2), (w3, b3) = layers
+    B, K = x.shape
+    N1, N2, N3 = w1.shape[0], w2.shape[0], w3.shape[0]
+    if x.stride(1) != 1 or w1.shape[1] != K or w2.shape[1] != N1 or w3.shape[1] != N2:
+        raise ValueError("pn2::fc_tail: x [B, K] with unit column stride and chained layer shapes")
+    nbytes = int(_L.pn2_fc_tail_workspace_bytes(B, N1, N2))
+    ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=x.device)
+    out = torch.empty(B, N3, dtype=torch.float32, device=x.device)
+    amax = torch.empty(B, dtype=torch.int64, device=x.device) if logsoftmax else None
+
+    def p(t):
+        return 0 if t is None else t.data_ptr()
+    _run("pn2_fc_tail_f32", _L.pn2_fc_tail_f32,
+         (x.data_ptr(), x.stride(0), B, K, w1.data_ptr(), p(b1), N1, w2.data_ptr(), p(b2), N2,
+          w3.data_ptr(), p(b3), N3, _lib.TAIL_LOGSOFTMAX if logsoftmax else 0, out.data_ptr(), N3,
+          p(amax), ws.data_ptr(), nbytes, _stream(x)), x.device,
+         flops=2.0 * B * (K * N1 + N1 * N2 + N2 * N3))
+    return out, amax

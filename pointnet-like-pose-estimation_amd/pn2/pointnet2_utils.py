@@ -245,9 +245,10 @@ class PointNetSetAbstraction(nn.Module):
         dev = pts.device
         if self.group_all:
             out = torch.empty(B, cout, device=dev, dtype=torch.float32)
+            # new_points = the reference's zeros (:136), filled by the MLP's last launch
+            new_points = torch.empty(B, C, 1, device=dev, dtype=torch.float32)
             ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_ALL, pts, feat, None, None, wts, als, bes, cins,
-                            splits, _precision(self))
-            new_points = torch.zeros(B, C, 1, device=dev, dtype=torch.float32)
+                                  splits, _precision(self), zero=new_points)
             return new_points, out.view(B, 1, cout).permute(0, 2, 1)
         S, K = self.point_number, self.sample_number
         pre = geometry.take(self, pts)  # FPS (+ ball query) precomputed by pn2.pipeline

@@ -233,3 +233,59 @@ def _group_all_vs_oracle(case, path):
     rows = pts.numpy() if feat is None else np.concatenate([pts.numpy(), feat.numpy()], -1)
     want = oracle.mlp_max(rows[:, None], _oracle_layers(sa.mlp_convs, sa.mlp_bns))  # [B, 1, cout]
     _close(newf.permute(0, 2, 1).cpu().numpy(), want)
+
+
+# The LDS-staged dense kernel (sa_dense.hip dense_lds_kernel: 64x64, 128x64 and 128x128 tiles by
+# the layer's size) vs dense_split_kernel: the same split, products and k order, so the same bits.
+# (C, D, N, mlp, B): SSG sa3 at the metric's B = 32 takes all three tiles (259->256 64x64,
+# 256->512 128x64, 512->1024 128x128 + LDS pool); translation_ssg's group_all pools over
+# K = 512 > 128 rows through HBM atomics; the v1 encoder's rows source below.
+DENSE_LDS = [
+    (3, 256, 128, [256, 512, 1024], 32),
+    (3, 256, 128, [256, 512, 1024], 5),
+    (10, 128, 512, [256, 512, 1024], 4),
+    (3, 64, 64, [64, 128], 3),
+]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", range(len(DENSE_LDS)))
+def test_dense_lds_matches_register_staged(case, prec):
+    import pn2
+    from pn2 import tuning
+    C, D, N, mlp, B = DENSE_LDS[case]
+    pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 700 + case)
+    feat = torch.randn(B, N, D, generator=torch.Generator().manual_seed(800 + case))
+    torch.manual_seed(case)
+    sa = pn2.PointNetSetAbstraction(None, None, None, C + D, mlp, True)
+    cases.randomize_bn(sa, case)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous().to(DEV)
+    f = feat.permute(0, 2, 1).contiguous().to(DEV)
+    outs = []
+    for lds in (1, 0):
+        with torch.no_grad(), pn2.mlp_precision(prec), tuning.override(dense_lds=lds):
+            outs.append(sa(x, f)[1].cpu().numpy())
+    np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    if prec == "fp32":
+        rows = np.concatenate([pts.numpy(), feat.numpy()], -1)
+        want = oracle.mlp_max(rows[:, None], _oracle_layers(sa.mlp_convs, sa.mlp_bns))
+        _close(outs[0].transpose(0, 2, 1), want)
+
+
+def test_dense_lds_rows_source_v1():
+    """PointNet-v1 encoder MLPs (rows source, unpooled and max over N = 1024 points, the last
+    layer signed / without ReLU): LDS-staged == register-staged bits."""
+    from pn2 import heads_v1, tuning
+    torch.manual_seed(5)
+    model = heads_v1.HEADS_V1["pointnet_cls"]()
+    cases.randomize_bn(model, 5)
+    model = model.to(DEV).eval()
+    x = cases.cloud("uniform3", 8, 1024, 9).permute(0, 2, 1).contiguous().to(DEV)
+    outs = []
+    for lds in (1, 0):
+        with torch.no_grad(), tuning.override(dense_lds=lds):
+            o = model(x)
+            outs.append([t.cpu().numpy() for t in (o if isinstance(o, tuple) else (o,)) if t is not None])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)

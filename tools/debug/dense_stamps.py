@@ -22,7 +22,7 @@ from pn2 import heads as H  # noqa: E402
 DEV = torch.device("cuda", 0)
 fn = _lib.load().pn2_debug_dense_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
-NW, NS = 4096, 16
+NW, NS = 4096, 18
 torch.manual_seed(8)
 pose = os.environ.get("CONFIG", "ssg") == "pose"  # translation_ssg B=64 N=2048: group_all over 32768 rows
 model = H.TranslationSSG().eval() if pose else H.ClsSSG().eval()
@@ -49,6 +49,8 @@ us = lambda v: v / 100.0
 nst = int(os.environ.get("NST", "8"))
 print("workgroups %d; entry spread p10/p50/p90/max %.2f %.2f %.2f %.2f us; span %.1f us" % (
     grid, *np.percentile(us(st[:, 0] - t0), [10, 50, 90, 100]), us(st[:, 15].max() - t0)))
+clk = (st[:, 17] - st[:, 16]) / np.maximum(1, st[:, 15] - st[:, 0]) * 100.0  # MHz
+print("in-kernel clock p10/p50/p90 %.0f %.0f %.0f MHz" % tuple(np.percentile(clk, [10, 50, 90])))
 rows = [("prologue", st[:, 1] - st[:, 0])]
 for c in range(1, nst):
     rows.append(("stage %d" % (c - 1), st[:, 1 + c] - st[:, c]))
