@@ -48,6 +48,7 @@ PEAK_F32_MFMA = 157.3  # TFLOP/s, MI355X_MICROARCH.md chip-level table (dense fp
 PEAK_BF16_MFMA = 16 * PEAK_F32_MFMA  # TFLOP/s, dense bf16 MFMA (2516.8)
 PEAK_SPLIT = PEAK_BF16_MFMA / 6  # fp32-equivalent ceiling of 6-product split-bf16 MFMA
 PEAK_HBM = 8000.0      # GB/s
+PEAK_F32_VALU = 157.3  # TFLOP/s, MI355X_MICROARCH.md (fp32 vector)
 
 CONFIGS = {
     # name: (head, clouds per GPU, points, cloud kind, description)
@@ -449,6 +450,22 @@ def main():
                 "avg_launch_ms": mlp["ms"] / mlp["launches"]}
     kernels = {k: {"ms_per_step": round(v["ms"] / a.steps, 4), "launches_per_step": v["launches"] / a.steps}
                for k, v in kern.items()}
+    # the north star's named kernel, query_ball_point: VALU-bound under compulsory-byte
+    # accounting; its HBM fraction is reported beside the VALU one
+    bq = kern.get("pn2_ball_query_f32")
+    roof_bq = None
+    if bq and bq["ms"] > 0:
+        t = bq["ms"] * 1e-3
+        roof_bq = {"bound": "valu", "achieved": round(bq["flops"] / t / 1e12, 3), "peak": PEAK_F32_VALU,
+                   "unit": "TFLOP/s", "frac": round(bq["flops"] / t / 1e12 / PEAK_F32_VALU, 4),
+                   "hbm_achieved": round(bq["bytes"] / t / 1e9, 1), "hbm_peak": PEAK_HBM,
+                   "hbm_unit": "GB/s", "hbm_frac": round(bq["bytes"] / t / 1e9 / PEAK_HBM, 4),
+                   "traffic": load_traffic(a.config, "pn2_ball_query_f32"),
+                   "kernel": "pn2_ball_query_f32 (ball_query_kernel)",
+                   "flops_basis": "algorithmic: every centroid-point pair x (2C+3) (SURVEY 8(d)); the "
+                                  "kernel stops a cloud's scan once all its centroids have K hits",
+                   "bytes_basis": "compulsory: packed points and centroids in, int64 [B,S,K] out",
+                   "avg_launch_ms": bq["ms"] / bq["launches"]}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.config == "ssg":
@@ -468,7 +485,7 @@ def main():
                         " + 7-way one-hot" if kind == "onehot10" else ""),
             "config": {"workload": desc, "global_batch": gB, "points": N, "heads": names,
                        "parallelism": "dp%d" % world},
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+            "roofline": roof, "roofline_ball_query": roof_bq, "cpu_baseline": cpu, "kernels": kernels,
             "launch": ("hip_graph" if a.graph else
                        "%s pipeline (fps%s stream%s)" % (
                            "eager" if a.eager_pipeline else "graphed",

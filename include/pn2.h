@@ -305,17 +305,17 @@ int pn2_linear_rows_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const
                         const float *bias, float *out, int64_t ldo, int64_t N, int flags,
                         void *stream);
 
-/* ---- the PointNet++ heads' eval FC tail in two launches: fc1 + bn1 + ReLU, fc2 + bn2 + ReLU,
- * fc3 (BN folded into W / bias on the host; dropout is the identity in eval), and with
- * PN2_TAIL_LOGSOFTMAX the classifiers' log_softmax over the N3 logits and the first argmax of
- * each row -- pointnet2_cls_ssg.py:31-38 (F.log_softmax(x, -1), x.data.max(1)[1]), the same
- * tails of pointnet2_cls_msg.py, rotation_ssg.py, translation_ssg.py, sign_ssg.py.  x [B][K]
- * (row stride ldx), W1 [N1][K], W2 [N2][N1], W3 [N3][N2] row-major; out [B][N3] (row stride
- * ldo): the log-probabilities with the flag, else the fc3 outputs; argmax [B] int64 or NULL.
- * fc1 and fc2 elements are computed as pn2_linear_rows_f32 computes them; each fc3 element is
- * a sequential float32 fma chain over k.  B * N3 <= 4096.  workspace:
- * pn2_fc_tail_workspace_bytes(B, N1, N2) bytes, 16-byte aligned (it holds an arrival ticket
- * the first launch zeroes; calls sharing a workspace must be stream-ordered). */
+/* ---- the PointNet++ heads' eval FC tail in three launches: fc1 + bn1 + ReLU, fc2 + bn2 + ReLU
+ * (as pn2_linear_rows_f32), then fc3 fused with the classifiers' log_softmax over the N3 logits
+ * and the first argmax of each row (PN2_TAIL_LOGSOFTMAX) -- pointnet2_cls_ssg.py:31-38
+ * (F.log_softmax(x, -1), x.data.max(1)[1]), the same tails of pointnet2_cls_msg.py,
+ * rotation_ssg.py, translation_ssg.py, sign_ssg.py.  BN is folded into W / bias on the host;
+ * dropout is the identity in eval.  x [B][K] (row stride ldx), W1 [N1][K], W2 [N2][N1],
+ * W3 [N3][N2] row-major; out [B][N3] (row stride ldo): the log-probabilities with the flag, else
+ * the fc3 outputs; argmax [B] int64 or NULL.  fc1 and fc2 elements are computed as
+ * pn2_linear_rows_f32 computes them; each fc3 element is the in-order sum of four float32 fma
+ * chains over consecutive quarters of k (the same whatever B is).  N3 <= 819.  workspace:
+ * pn2_fc_tail_workspace_bytes(B, N1, N2) bytes, 16-byte aligned (y1 and y2). */
 #define PN2_TAIL_LOGSOFTMAX 1
 int64_t pn2_fc_tail_workspace_bytes(int64_t B, int64_t N1, int64_t N2);
 int pn2_fc_tail_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const float *W1,

@@ -141,89 +141,146 @@ __global__ __launch_bounds__(64 * kLinWaves) void linear_rows_kernel(const float
                                                                      const float *__restrict__ W,
                                                                      const float *__restrict__ bias,
                                                                      float *__restrict__ out, int64_t ldo,
-                                                                     int64_t N, int relu, int vec,
-                                                                     unsigned *zero_word) {
-    // side job: reset the next launch's arrival ticket (fc_tail), published by stream order
-    if (zero_word && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *zero_word = 0u;
+                                                                     int64_t N, int relu, int vec) {
     linear_rows_block<BT>(x, ldx, B, K, W, bias, out, ldo, N, relu, vec);
 }
 
-// ---- the heads' FC tail, second half: fc2 (+ folded BN, ReLU) over the grid as
-// linear_rows_kernel, then the workgroup that finishes last computes fc3 for every row and, with
+// ---- the heads' FC tail, last layer: fc3 for kTailRows rows per workgroup and, with
 // PN2_TAIL_LOGSOFTMAX, log_softmax and the first argmax of each row (pointnet2_cls_ssg.py:36-38:
-// F.log_softmax(x, -1) and x.data.max(1)[1]).  fc3 element (b, n) is one thread's sequential
-// fma chain over k (the same whatever the row count: sharded batches stay bit-identical).
-// Hand-off: every workgroup's y2 stores -> vmcnt(0) -> barrier -> agent release -> ticket
-// fetch_add; the last arriver acquires before reading y2 (MI355X_MICROARCH.md, inter-workgroup
-// visibility), and resets the ticket for the next launch (the fc1 launch also zeroes it first).
-constexpr int kTailMaxLogits = 4096;  // B * N3 staged in LDS for the softmax
+// F.log_softmax(x, -1) and x.data.max(1)[1]) -- one launch, after fc1 and fc2 as
+// linear_rows_kernel launches.  (An in-launch fc2 -> fc3 seam, an arrival ticket with the last
+// workgroup computing fc3, cost 10-15 us over the separate launches: the fan-in of the ~128
+// arrivals and their skew; MI355X_MICROARCH.md's splitk-seam / fanin rows.)
+// fc3 element (b, n) is the in-order sum of kTailKS partial fma chains over consecutive
+// segments of k: one thread per (n, segment) holds the workgroup's kTailRows rows, its weight
+// segment read once.  The order depends on the shape only, never on the row count (sharded
+// batches stay bit-identical).
+constexpr int kTailKS = 4, kTailRows = 4;
+constexpr int kTailT = 256;
 
-template <int BT>
-__global__ __launch_bounds__(64 * kLinWaves) void fc23_kernel(
-    const float *__restrict__ y1, int64_t ld1, int B, int64_t K2, const float *__restrict__ W2,
-    const float *__restrict__ b2, float *__restrict__ y2, int64_t N2, const float *__restrict__ W3,
-    const float *__restrict__ b3, int N3, int flags, float *__restrict__ out, int64_t ldo,
-    int64_t *__restrict__ amax, unsigned *ticket, int vec) {
-    __shared__ float logits[kTailMaxLogits];
-    __shared__ int is_last;
-    linear_rows_block<BT>(y1, ld1, B, K2, W2, b2, y2, N2, N2, 1, vec);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = t == gridDim.x * gridDim.y - 1;
-    }
-    __syncthreads();
-    if (!is_last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    const int tot = B * N3;
-    const bool vec3 = vec && (N2 & 3) == 0 && (reinterpret_cast<uintptr_t>(W3) & 15) == 0;
-    for (int e = threadIdx.x; e < tot; e += 64 * kLinWaves) {
-        const int b = e / N3, n = e - b * N3;
-        const float *xr = y2 + (int64_t)b * N2, *wr = W3 + (int64_t)n * N2;
-        float a = 0.f;
-        if (vec3) {
-            for (int64_t k = 0; k < N2; k += 4) {
-                const float4 xv = *reinterpret_cast<const float4 *>(xr + k);
-                const float4 wv = *reinterpret_cast<const float4 *>(wr + k);
-                a = fmaf(wv.x, xv.x, a);
-                a = fmaf(wv.y, xv.y, a);
-                a = fmaf(wv.z, xv.z, a);
-                a = fmaf(wv.w, xv.w, a);
+template <bool VEC>
+__global__ __launch_bounds__(kTailT) void fc3_tail_kernel(const float *__restrict__ y2, int B, int64_t N2,
+                                                          const float *__restrict__ W3,
+                                                          const float *__restrict__ b3, int N3, int flags,
+                                                          float *__restrict__ out, int64_t ldo,
+                                                          int64_t *__restrict__ amax) {
+    extern __shared__ __attribute__((aligned(16))) float tsm[];
+    float *logits = tsm;                          // [kTailRows][N3]
+    float *part = tsm + kTailRows * N3;           // [kTailKS][kTailRows][N3]
+    float *sy = part + kTailKS * kTailRows * N3;  // VEC: [kTailRows][N2], 16-byte aligned
+    const int r0 = (int)blockIdx.x * kTailRows;
+    const int R = B - r0 < kTailRows ? B - r0 : kTailRows;
+    y2 += (int64_t)r0 * N2;
+    out += (int64_t)r0 * ldo;
+    const int64_t kl = VEC ? N2 / kTailKS : (N2 + kTailKS - 1) / kTailKS;
+    const int items = N3 * kTailKS;
+    if constexpr (VEC) {
+        // one round trip: the thread's first weight chunk (kC float4 of its row segment) in
+        // flight together with the rows' y2 staging into LDS; lanes then read y2 from LDS at one
+        // address per k (a broadcast)
+        constexpr int kC = 16;
+        float4 w[kC];
+        auto load_w = [&](int it, int64_t kb) {
+            const int n = it % N3, q = it / N3;
+            const int64_t k1 = q * kl + kl;
+            const float *wr = W3 + (int64_t)n * N2;
+#pragma unroll
+            for (int u = 0; u < kC; ++u) {
+                const int64_t k = kb + 4 * u < k1 ? kb + 4 * u : k1 - 4;  // clamped, not used
+                w[u] = *reinterpret_cast<const float4 *>(wr + k);
             }
-        } else {
-            for (int64_t k = 0; k < N2; ++k) a = fmaf(wr[k], xr[k], a);
+        };
+        if ((int)threadIdx.x < items) load_w(threadIdx.x, (threadIdx.x / N3) * kl);
+        const float4 *y4 = reinterpret_cast<const float4 *>(y2);
+        for (int64_t e = threadIdx.x; e < (int64_t)R * N2 / 4; e += kTailT) reinterpret_cast<float4 *>(sy)[e] = y4[e];
+        __syncthreads();
+        for (int it = threadIdx.x; it < items; it += kTailT) {
+            const int n = it % N3, q = it / N3;
+            const int64_t k0 = q * kl, k1 = k0 + kl;
+            float acc[kTailRows];
+#pragma unroll
+            for (int i = 0; i < kTailRows; ++i) acc[i] = 0.f;
+            for (int64_t kb = k0; kb < k1; kb += 4 * kC) {
+                if (it != (int)threadIdx.x || kb != k0) load_w(it, kb);
+#pragma unroll
+                for (int u = 0; u < kC; ++u)
+                    if (kb + 4 * u < k1)
+#pragma unroll
+                        for (int i = 0; i < kTailRows; ++i) {
+                            const float4 y =
+                                *reinterpret_cast<const float4 *>(sy + (int64_t)(i < R ? i : R - 1) * N2 + kb + 4 * u);
+                            float a = acc[i];
+                            a = fmaf(w[u].x, y.x, a);
+                            a = fmaf(w[u].y, y.y, a);
+                            a = fmaf(w[u].z, y.z, a);
+                            a = fmaf(w[u].w, y.w, a);
+                            acc[i] = a;
+                        }
+            }
+#pragma unroll
+            for (int i = 0; i < kTailRows; ++i) part[(q * kTailRows + i) * N3 + n] = acc[i];
         }
+    } else {
+        const float *yr[kTailRows];
+#pragma unroll
+        for (int i = 0; i < kTailRows; ++i) yr[i] = y2 + (int64_t)(i < R ? i : R - 1) * N2;
+        for (int it = threadIdx.x; it < items; it += kTailT) {
+            const int n = it % N3, q = it / N3;
+            const int64_t k0 = q * kl, k1 = k0 + kl < N2 ? k0 + kl : N2;
+            const float *wr = W3 + (int64_t)n * N2;
+            float acc[kTailRows];
+#pragma unroll
+            for (int i = 0; i < kTailRows; ++i) acc[i] = 0.f;
+            for (int64_t k = k0; k < k1; ++k) {
+                const float w = wr[k];
+#pragma unroll
+                for (int i = 0; i < kTailRows; ++i) acc[i] = fmaf(w, yr[i][k], acc[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < kTailRows; ++i) part[(q * kTailRows + i) * N3 + n] = acc[i];
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < R * N3; e += kTailT) {
+        const int b = e / N3, n = e - b * N3;
+        float a = part[e];
+#pragma unroll
+        for (int q = 1; q < kTailKS; ++q) a += part[q * kTailRows * N3 + e];
         a += b3 ? b3[n] : 0.f;
         if (flags & PN2_TAIL_LOGSOFTMAX) logits[e] = a;
         else out[(int64_t)b * ldo + n] = a;
     }
     if (flags & PN2_TAIL_LOGSOFTMAX) {
         __syncthreads();
-        for (int b = threadIdx.x; b < B; b += 64 * kLinWaves) {
+        // one wave per row: max, sum of exp and the first argmax as wave reductions
+        const int lane = threadIdx.x & 63, wave = threadIdx.x / 64;
+        for (int b = wave; b < R; b += kTailT / 64) {
             const float *v = logits + b * N3;
-            float m = v[0];
-            for (int n = 1; n < N3; ++n) m = fmaxf(m, v[n]);
-            float s = 0.f;
-            for (int n = 0; n < N3; ++n) s += expf(v[n] - m);
-            const float ls = logf(s);
-            float best = 0.f;
-            int bi = 0;
-            for (int n = 0; n < N3; ++n) {
+            float m = -INFINITY;
+            for (int n = lane; n < N3; n += 64) m = fmaxf(m, v[n]);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+            float sum = 0.f;
+            for (int n = lane; n < N3; n += 64) sum += expf(v[n] - m);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+            const float ls = logf(sum);
+            float best = -INFINITY;
+            int bi = N3;
+            for (int n = lane; n < N3; n += 64) {
                 const float o = (v[n] - m) - ls;
                 out[(int64_t)b * ldo + n] = o;
-                if (n == 0 || o > best) best = o, bi = n;
+                if (o > best) best = o, bi = n;  // the lane's first maximum
             }
-            if (amax) amax[b] = bi;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {  // the first index among equal maxima
+                const float ob = __shfl_xor(best, o);
+                const int oi = __shfl_xor(bi, o);
+                if (ob > best || (ob == best && oi < bi)) best = ob, bi = oi;
+            }
+            if (amax && lane == 0) amax[r0 + b] = bi < N3 ? bi : 0;
         }
     }
-    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace pn2
@@ -248,10 +305,10 @@ extern "C" int pn2_linear_rows_f32(const float *x, int64_t ldx, int64_t B, int64
     const dim3 block(64 * kLinWaves);
     if (B <= 8)
         hipLaunchKernelGGL(linear_rows_kernel<8>, grid(lin_rows<8>(), 8), block, 0, st, x, ldx, (int)B, K, W, bias,
-                           out, ldo, N, relu, vec, nullptr);
+                           out, ldo, N, relu, vec);
     else
         hipLaunchKernelGGL(linear_rows_kernel<16>, grid(lin_rows<16>(), 16), block, 0, st, x, ldx, (int)B, K, W, bias,
-                           out, ldo, N, relu, vec, nullptr);
+                           out, ldo, N, relu, vec);
     PN2_LAUNCH_CHECK("linear_rows_kernel");
     return PN2_OK;
 }
@@ -262,7 +319,7 @@ static int64_t tail_ws_floats(int64_t B, int64_t N1, int64_t N2) {
 
 extern "C" int64_t pn2_fc_tail_workspace_bytes(int64_t B, int64_t N1, int64_t N2) {
     if (B < 1 || N1 < 1 || N2 < 1) return -1;
-    return tail_ws_floats(B, N1, N2) * 4 + 16;
+    return tail_ws_floats(B, N1, N2) * 4;
 }
 
 extern "C" int pn2_fc_tail_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const float *W1,
@@ -274,32 +331,28 @@ extern "C" int pn2_fc_tail_f32(const float *x, int64_t ldx, int64_t B, int64_t K
     PN2_REQUIRE(B >= 1 && (B + 15) / 16 <= 65535 && K >= 1 && N1 >= 1 && N2 >= 1 && N3 >= 1 &&
                     ldx >= K && ldo >= N3, "pn2_fc_tail_f32: bad shape");
     PN2_REQUIRE((flags & ~PN2_TAIL_LOGSOFTMAX) == 0, "pn2_fc_tail_f32: unknown flags");
-    PN2_REQUIRE(B * N3 <= kTailMaxLogits, "pn2_fc_tail_f32: B*N3 = %lld exceeds %d", (long long)(B * N3),
-                kTailMaxLogits);
+    const size_t lds = (size_t)(1 + kTailKS) * kTailRows * N3 * 4;
+    PN2_REQUIRE(lds <= 64 * 1024, "pn2_fc_tail_f32: N3 = %lld exceeds %d", (long long)N3,
+                64 * 1024 / (4 * (1 + kTailKS) * kTailRows));
+    const size_t lds_vec = (lds + 15) / 16 * 16 + (size_t)kTailRows * N2 * 4;  // + the y2 rows
     PN2_REQUIRE(workspace_bytes >= pn2_fc_tail_workspace_bytes(B, N1, N2) && ((uintptr_t)workspace & 15) == 0,
                 "pn2_fc_tail_f32: workspace too small or not 16-byte aligned");
     float *y1 = reinterpret_cast<float *>(workspace);
     float *y2 = y1 + (B * N1 + 3) / 4 * 4;
-    unsigned *ticket = reinterpret_cast<unsigned *>(y1 + tail_ws_floats(B, N1, N2));
+    if (const int rc = pn2_linear_rows_f32(x, ldx, B, K, W1, b1, y1, N1, N1, PN2_LINEAR_RELU, stream)) return rc;
+    if (const int rc = pn2_linear_rows_f32(y1, N1, B, N1, W2, b2, y2, N2, N2, PN2_LINEAR_RELU, stream)) return rc;
+    // 16-byte loads when the weight rows and the y2 rows are 16-byte aligned and k splits into
+    // kTailKS segments of whole float4s (a shape-only choice: the summation order with it)
+    const bool vec = (reinterpret_cast<uintptr_t>(W3) & 15) == 0 && N2 % (4 * kTailKS) == 0 &&
+                     lds_vec <= 64 * 1024;
+    const dim3 grid((unsigned)((B + kTailRows - 1) / kTailRows)), block(kTailT);
     hipStream_t st = as_stream(stream);
-    const int vec1 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W1)) & 15) == 0 &&
-                     (K & 3) == 0 && (ldx & 3) == 0;
-    const int vec2 = (reinterpret_cast<uintptr_t>(W2) & 15) == 0 && (N1 & 3) == 0;
-    auto grid = [B](int64_t N, int rows, int bt) {
-        return dim3((unsigned)((N + rows - 1) / rows), (unsigned)((B + bt - 1) / bt));
-    };
-    const dim3 block(64 * kLinWaves);
-    if (B <= 8) {
-        hipLaunchKernelGGL(linear_rows_kernel<8>, grid(N1, lin_rows<8>(), 8), block, 0, st, x, ldx, (int)B, K, W1,
-                           b1, y1, N1, N1, 1, vec1, ticket);
-        hipLaunchKernelGGL(fc23_kernel<8>, grid(N2, lin_rows<8>(), 8), block, 0, st, y1, N1, (int)B, N1, W2, b2,
-                           y2, N2, W3, b3, (int)N3, flags, out, ldo, argmax, ticket, vec2);
-    } else {
-        hipLaunchKernelGGL(linear_rows_kernel<16>, grid(N1, lin_rows<16>(), 16), block, 0, st, x, ldx, (int)B, K,
-                           W1, b1, y1, N1, N1, 1, vec1, ticket);
-        hipLaunchKernelGGL(fc23_kernel<16>, grid(N2, lin_rows<16>(), 16), block, 0, st, y1, N1, (int)B, N1, W2, b2,
-                           y2, N2, W3, b3, (int)N3, flags, out, ldo, argmax, ticket, vec2);
-    }
-    PN2_LAUNCH_CHECK("fc23_kernel");
+    if (vec)
+        hipLaunchKernelGGL(fc3_tail_kernel<true>, grid, block, lds_vec, st, y2, (int)B, N2, W3, b3, (int)N3, flags, out,
+                           ldo, argmax);
+    else
+        hipLaunchKernelGGL(fc3_tail_kernel<false>, grid, block, lds, st, y2, (int)B, N2, W3, b3, (int)N3, flags, out,
+                           ldo, argmax);
+    PN2_LAUNCH_CHECK("fc3_tail_kernel");
     return PN2_OK;
 }

@@ -807,12 +807,13 @@ static int launch_dense_lds_ns(DenseSplitArgs A, hipStream_t st) {
     return PN2_OK;
 }
 
-// ring depth: tuning dense_lds_stages (3 or 4; 4 only where four stages fit the CU's LDS)
+// ring depth: tuning dense_lds_stages (2, 3 or 4; 4 only where four stages fit the CU's LDS)
 template <int WR, int NTW, int NP>
 static int launch_dense_lds(const DenseSplitArgs &A, hipStream_t st) {
     constexpr size_t stage = (size_t)32 * WR * 128 + (size_t)2 * NTW * NP * 1024;
     if constexpr (4 * stage <= 160 * 1024)
         if (tuning().dense_lds_stages >= 4) return launch_dense_lds_ns<WR, NTW, NP, 4>(A, st);
+    if (tuning().dense_lds_stages <= 2) return launch_dense_lds_ns<WR, NTW, NP, 2>(A, st);
     return launch_dense_lds_ns<WR, NTW, NP, 3>(A, st);
 }
 

@@ -26,15 +26,15 @@ from .pointnet2_utils import PointNetSetAbstraction as SA
 from .pointnet2_utils import PointNetSetAbstractionMsg as SAMsg
 from .pointnet2_utils import _needs_autograd
 from . import ops
+from . import tuning
 from .pointnet_utils import _fold_linear, linear_bn
 
 
 class _FCHead(nn.Module):
     """fc1/bn1/relu/drop -> fc2/bn2/relu/drop -> fc3, shared by every head.  Eval without
-    autograd: each fc + bn folded into one (W', b') and the whole tail in two launches
-    (pn2.ops.fc_tail: fc1 over the grid, then fc2 over the grid and fc3 -- with the
-    classifiers' log_softmax and argmax -- in its last workgroup; dropout is the identity in
-    eval).  Otherwise, or when a layer cannot fold, the reference's modules."""
+    autograd: each fc + bn folded into one (W', b') and the whole tail in three launches
+    (pn2.ops.fc_tail: fc1 and fc2 as row kernels, then fc3 fused with the classifiers'
+    log_softmax and argmax; dropout is the identity in eval).  Otherwise, or when a layer cannot fold, the reference's modules."""
 
     def _folded(self):
         c = self._fc_cache
@@ -44,8 +44,8 @@ class _FCHead(nn.Module):
         return None if any(t is None for t in wb) else wb
 
     def _fused_ok(self, x):
-        return (not _needs_autograd(self, x) and x.is_cuda and x.dtype == torch.float32 and
-                x.dim() == 2 and x.stride(1) == 1 and x.shape[0] * self.fc3.out_features <= 4096)
+        return (tuning.get("fc_tail") and not _needs_autograd(self, x) and x.is_cuda and x.dtype == torch.float32 and
+                x.dim() == 2 and x.stride(1) == 1 and self.fc3.out_features <= 819)
 
     def _fc(self, x):
         if self._fused_ok(x):

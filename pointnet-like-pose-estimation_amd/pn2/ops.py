@@ -192,7 +192,8 @@ def ball_query_direct(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: fl
     _run("pn2_ball_query_f32", _L.pn2_ball_query_cnt_f32,
          (pts_packed.data_ptr(), ctr_packed.data_ptr(), B, N, S, C, float(radius), nsample,
           out.data_ptr(), 0 if cnt is None else cnt.data_ptr(), _stream(pts_packed)),
-         pts_packed.device, nbytes=4.0 * cp * B * (N + S) + 8.0 * B * S * nsample)
+         pts_packed.device, nbytes=4.0 * cp * B * (N + S) + 8.0 * B * S * nsample,
+         flops=float(B) * S * N * (2 * C + 3))  # pairs x (2C + 3)
     return (out, cnt) if with_count else out
 
 

@@ -16,6 +16,8 @@ Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_s
     drain_heads      how many final batches of a pipelined run take their heads on their own
                      compute streams (default 2)
     geometry_stream  1: the eager forward runs layer i+1's FPS + ball query on a side stream
+    fc_tail          0: the heads' FC tail as one row-kernel launch per layer + torch's
+                     log_softmax / argmax, instead of pn2_fc_tail_f32's fused fc3 + log_softmax
 
 Unknown keys are an error.  ``override(**kw)`` changes keys for the duration of a ``with``
 block (tests).  Every default is the measured best.
@@ -30,6 +32,7 @@ HOST_DEFAULTS = {
     "pipe_split_last": 0,
     "drain_heads": 2,
     "geometry_stream": 0,
+    "fc_tail": 1,
 }
 
 

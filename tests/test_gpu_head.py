@@ -33,7 +33,7 @@ def _ref_tail(m, x):
     return y @ md["fc3.weight"].T + md["fc3.bias"]
 
 
-@pytest.mark.parametrize("B", [1, 5, 32, 64])
+@pytest.mark.parametrize("B", [1, 5, 20, 32, 64])
 @pytest.mark.parametrize("head", ["ClsSSG", "RotationSSG", "SignSSG"])
 def test_fc_tail_matches_reference(head, B):
     m = _model(head, 11).to(DEV)
@@ -68,8 +68,7 @@ def test_fc_tail_rows_independent_of_batch():
 
 
 def test_fc_tail_repeated_calls_same_bits():
-    """The arrival ticket resets between launches: back-to-back calls on one stream (and a
-    graph replay) agree."""
+    """Back-to-back calls on one stream and a graph replay give the same bits."""
     m = _model("ClsSSG", 6).to(DEV)
     x = torch.relu(torch.randn(32, 1024, generator=torch.Generator().manual_seed(1))).to(DEV)
     with torch.no_grad():
@@ -106,3 +105,24 @@ def test_group_all_new_points_zero_filled():
         newp, _ = sa(pts, feat)
     assert newp.shape == (8, 3, 1)
     assert torch.equal(newp, torch.zeros_like(newp))
+
+
+def test_fc_tail_argmax_first_of_ties():
+    """Equal logits: the first index wins (x.data.max(1)[1] on the reference's CPU tensors), also
+    when the tie spans the wave's lanes (40 classes, one per lane)."""
+    from pn2 import heads as H
+    torch.manual_seed(8)
+    m = H.ClsSSG(num_category=40)
+    cases.randomize_bn(m, 8)
+    m.eval()
+    with torch.no_grad():
+        m.fc3.weight.zero_()
+        m.fc3.bias.zero_()
+        m.fc3.bias[[7, 13, 30]] = 1.0
+    m = m.to(DEV)
+    with torch.no_grad():
+        x = torch.relu(torch.randn(6, 1024, generator=torch.Generator().manual_seed(3))).to(DEV)
+        logp, pred = m._fc_log_softmax(x)
+    assert pred.tolist() == [7] * 6
+    want = torch.log_softmax(m.fc3.bias.detach().double().cpu(), 0)
+    np.testing.assert_allclose(logp.cpu().double().numpy(), want.expand(6, -1).numpy(), rtol=1e-6, atol=1e-6)

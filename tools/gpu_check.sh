@@ -26,13 +26,15 @@ for s in $STEPS; do
     pmc)
       # one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one gfx950 TCC pass);
       # eager launch so every kernel runs on the full chip, as the kernel timer measures it
-      for c in FETCH_SIZE WRITE_SIZE; do
-        rm -rf $OUT/pmc_$c
-        timeout -k 10 300 rocprofv3 --pmc $c -d $OUT/pmc_$c -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timer --no-pipeline > $OUT/pmc_$c.log 2>&1; ok $? pmc_$c
+      for cfg in ${PMC_CONFIGS:-ssg}; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          rm -rf $OUT/pmc_${cfg}_$c
+          timeout -k 10 300 rocprofv3 --pmc $c -d $OUT/pmc_${cfg}_$c -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timer --no-pipeline > $OUT/pmc_${cfg}_$c.log 2>&1; ok $? pmc_${cfg}_$c
+        done
+        python tools/pmc_traffic.py $OUT/pmc_${cfg}_FETCH_SIZE $OUT/pmc_${cfg}_WRITE_SIZE --config $cfg > $OUT/pmc_summary_$cfg.txt 2>&1
+        head -3 $OUT/pmc_summary_$cfg.txt
       done
-      python tools/pmc_traffic.py $OUT/pmc_FETCH_SIZE $OUT/pmc_WRITE_SIZE --config ssg > $OUT/pmc_summary.txt 2>&1
-      cp profiles/pmc_traffic.json $OUT/pmc_traffic.json
-      head -3 $OUT/pmc_summary.txt ;;
+      cp profiles/pmc_traffic.json $OUT/pmc_traffic.json ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -40,7 +40,7 @@ __device__ __forceinline__ floatx16 mma6(const Split &x, const Split &w, floatx1
 // MODE 0: MFMAs only (operands fixed in registers); 1: + LDS reads and split per iteration;
 // 2: + s_barrier per iteration
 template <int MODE>
-__global__ void k(const float *in, floatx16 *out, long long *cyc, int iters) {
+__global__ __launch_bounds__(1024) void k(const float *in, floatx16 *out, long long *cyc, int iters) {
     __shared__ __attribute__((aligned(16))) char lds[65536];
     const int lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 65536 / 4; i += blockDim.x) reinterpret_cast<float *>(lds)[i] = in[i & 1023];
@@ -89,25 +89,34 @@ int main() {
     float hin[4096];
     for (int i = 0; i < 4096; ++i) hin[i] = (float)((i * 2654435761u) % 1000) / 997.f - 0.5f;
     hipMemcpy(in, hin, sizeof(hin), hipMemcpyHostToDevice);
-    hipMalloc(&out, 256 * 512 * 64);
+    hipMalloc(&out, (size_t)256 * 1024 * 64);  // up to 1024 threads per block, one floatx16 each
     hipMalloc(&cyc, 256 * 8);
     const int iters = 4000;
     long long h[256];
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
     for (int mode = 0; mode < 3; ++mode)
-        for (int waves = 4; waves <= 8; waves += 4) {
+        for (int waves = 4; waves <= (mode == 0 ? 16 : 8); waves += 4) {
+            float ms = 0.f;
             for (int rep = 0; rep < 2; ++rep) {
+                hipEventRecord(e0, 0);
                 if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(256), dim3(64 * waves), 0, 0, in, out, cyc, iters);
                 if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(256), dim3(64 * waves), 0, 0, in, out, cyc, iters);
                 if (mode == 2) hipLaunchKernelGGL(k<2>, dim3(256), dim3(64 * waves), 0, 0, in, out, cyc, iters);
+                hipEventRecord(e1, 0);
                 hipDeviceSynchronize();
+                hipEventElapsedTime(&ms, e0, e1);
             }
             hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
             double s = 0;
             for (int i = 0; i < 256; ++i) s += h[i];
             const double per_it = s / 256 / iters;
             // MFMA cycles per SIMD and iteration: waves/4 waves x 24 MFMAs x 32 cycles
-            printf("mode %d waves/SIMD %d: %.0f cycles/iteration, MFMA-pipe floor %d (%.0f%%)\n", mode, waves / 4,
-                   per_it, waves / 4 * 24 * 32, 100.0 * waves / 4 * 24 * 32 / per_it);
+            const double flops = 256.0 * waves * iters * 24 * 32768.0;
+            printf("mode %d waves/SIMD %d: %.0f cycles/iteration, 32-cycle floor %d (%.0f%%); %.3f ms = %.0f TFLOP/s bf16\n",
+                   mode, waves / 4, per_it, waves / 4 * 24 * 32, 100.0 * waves / 4 * 24 * 32 / per_it, ms,
+                   flops / (ms * 1e-3) / 1e12);
         }
     return 0;
 }

@@ -24,8 +24,12 @@ CALLS_PER_FORWARD = {"ssg": 3, "msg": 7, "pose": 6, "stress": 3}
 FORWARD_MARKER = "fps_kernel"  # one launch per sampled SA layer, counted below
 # kernels one pn2_sa_mlp_max_f32 call may dispatch
 MLP_KERNELS = ("sa_mlp_kernel", "dense_layer_kernel", "sa_chain_kernel", "dense_split_kernel",
-               "compact_scan_kernel", "u_table_kernel")
+               "dense_lds_kernel", "compact_scan_kernel", "u_table_kernel", "unkey_kernel")
 FPS_PER_FORWARD = {"ssg": 2, "msg": 2, "pose": 4, "stress": 2}
+# pn2_ball_query_f32 calls per forward (one per radius of every grouping SA layer)
+BQ_PER_FORWARD = {"ssg": 2, "msg": 6, "pose": 3, "stress": 2}
+# the MLP entry point each config's bench line names (config 5 runs the bf16 MLP)
+MLP_NAME = {"stress": "pn2_sa_mlp_max_bf16"}
 
 
 def read(d, counter):
@@ -71,9 +75,13 @@ def main():
         if any(k in name for k in MLP_KERNELS):
             mlp_total += 1024 * sum(v)
     per_call = mlp_total / (forwards * CALLS_PER_FORWARD[a.config]) if forwards else None
+    bq_total = sum(2 * 1024 * sum(v) for k, v in fetch.items() if "ball_query_kernel" in k) + \
+        sum(1024 * sum(v) for k, v in write.items() if "ball_query_kernel" in k)
+    bq_call = bq_total / (forwards * BQ_PER_FORWARD[a.config]) if forwards else None
     out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    data[a.config] = {"pn2_sa_mlp_max_f32": per_call, "forwards": forwards, "kernels": kernels,
+    data[a.config] = {MLP_NAME.get(a.config, "pn2_sa_mlp_max_f32"): per_call,
+                      "pn2_ball_query_f32": bq_call, "forwards": forwards, "kernels": kernels,
                       "note": "bytes per dispatch; FETCH_SIZE x2 (gfx950), KB->bytes"}
     json.dump(data, open(out_path, "w"), indent=1, sort_keys=True)
     print(json.dumps({"config": a.config, "per_call_bytes": per_call, "forwards": forwards}))
