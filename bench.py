@@ -437,6 +437,7 @@ def main():
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1),
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                 "traffic": load_traffic(a.config, mlp_name),
+                "compulsory_bytes_per_launch": mlp["bytes"] / mlp["launches"],
                 "kernel": "%s (sa_chain_kernel / dense_split_kernel, %s)" % (
                     mlp_name, "bf16, 1 MFMA per product" if prec == "bf16" else "split-bf16"),
                 "fp32_mfma_peak": PEAK_F32_MFMA,
@@ -448,6 +449,8 @@ def main():
                                "only each group's distinct neighbour rows), so achieved and "
                                "frac are effective rates",
                 "avg_launch_ms": mlp["ms"] / mlp["launches"]}
+        if roof["traffic"]:
+            roof["traffic_vs_compulsory"] = round(roof["traffic"] / roof["compulsory_bytes_per_launch"], 2)
     kernels = {k: {"ms_per_step": round(v["ms"] / a.steps, 4), "launches_per_step": v["launches"] / a.steps}
                for k, v in kern.items()}
     # the north star's named kernel, query_ball_point: VALU-bound under compulsory-byte

@@ -16,6 +16,7 @@
  *
  * Reference interfaces replaced (file:line in /root/reference):
  *   pn2_fps_f32            farthest_point_sample            model/pointnet2_utils.py:47-68
+ *   pn2_fps_ws_f32         the same, any N (workspace)       model/pointnet2_utils.py:47-68
  *                          (+ index_points(points, fps_idx)  model/pointnet2_utils.py:106)
  *   pn2_ball_query_f32     query_ball_point + square_distance model/pointnet2_utils.py:70-90, 5-26
  *   pn2_pack_points_f32    torch.sum(points**2,-1) of square_distance model/pointnet2_utils.py:24-25
@@ -57,7 +58,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 10
+#define PN2_ABI_VERSION 11
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -95,12 +96,22 @@ int64_t pn2_packed_stride(int64_t C);
  *   out_pts    [B,S,C] float32 contiguous, or NULL   index_points(points, fps_idx)
  *   out_packed [B,S,cp] float32, or NULL         packed centroids (contiguous-layout ssq)
  *   pts_packed [B,N,cp] float32, or NULL         packed input points (input-layout ssq)
- * N <= 16384 and C <= 16 (else PN2_EUNSUPPORTED); S <= 8192.  The cloud is register-resident
- * up to N = 16384 for C == 3, 8192 for C == 10, 4096 for other C; past that the channels after
- * xyz are re-read from pts each iteration unless they are constant over the cloud (one-hot). */
+ * C <= 16 (else PN2_EUNSUPPORTED: the channel-sum orders pinned against the reference are
+ * those of C <= 16).  The cloud is register-resident up to N = 16384 for C == 3, 8192 for
+ * C == 10, 4096 for other C (past that, up to N = 16384, the channels after xyz are re-read
+ * from pts each iteration unless they are constant over the cloud: one-hot), with S <= 8192.
+ * Any other N or S runs the streamed kernel: the points re-read every iteration, the running
+ * distances in LDS up to N = 40952, past that in a caller workspace of
+ * pn2_fps_workspace_bytes(B, N, C, S) bytes (pn2_fps_ws_f32; pn2_fps_f32 passes none and
+ * fails with PN2_EINVAL when one is needed). */
 int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
                 int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
                 float *out_packed, float *pts_packed, void *stream);
+int64_t pn2_fps_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t S);
+int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+                   int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
+                   float *out_packed, float *pts_packed, void *workspace, int64_t workspace_bytes,
+                   void *stream);
 
 /* Pack a [B,N,C] strided view into [B,N,cp] with its ssq (see above). */
 int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,

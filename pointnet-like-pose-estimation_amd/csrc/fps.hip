@@ -307,6 +307,125 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
     }
 }
 
+// ------------------------------------------------------------------------- streamed FPS
+// Any N and S: nothing of the cloud is register-resident.  Each iteration every thread walks
+// the points n = tid, tid + NT, ... (coalesced reads of the input for either layout), computes
+// the distance in the reference's order, updates the running minimum -- held in LDS when the
+// cloud's N words fit (DL), else in the caller's workspace (one word per point) -- and keeps
+// the 64-bit key (distance bits : ~index), whose maximum is torch.max's first index among the
+// maxima.  Wave max by shuffles, one LDS slot per wave (double-buffered by parity), ONE
+// barrier, every thread reduces the NW slots.  The centroid's coordinates are re-read from
+// the input (one broadcast load).  Indices go straight to out_idx; the output pass reads them
+// back with sc1 loads (stores of other waves of this workgroup).
+constexpr int kFpsStreamT = 1024;
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const unsigned long long w = __shfl_xor(v, o);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
+template <int CM, bool FIXED, bool DL>
+__global__ __launch_bounds__(kFpsStreamT) void fps_stream_kernel(
+    const float *__restrict__ pts, int N, int Crt, int64_t sb, int64_t sn, int64_t sc, int kind,
+    const int64_t *__restrict__ start, int S, int64_t *__restrict__ out_idx, float *__restrict__ out_pts,
+    float *__restrict__ out_packed, float *__restrict__ pts_packed, int cp, unsigned *__restrict__ dist_ws) {
+    constexpr int NT = kFpsStreamT, NW = NT / 64;
+    __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
+    const int C = FIXED ? CM : Crt;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x;
+    const float *P = pts + (int64_t)b * sb;
+    extern __shared__ __attribute__((aligned(16))) unsigned long long ssm[];
+    unsigned long long *slots = ssm;                               // [2][NW]
+    unsigned *dist = DL ? reinterpret_cast<unsigned *>(ssm + 2 * NW)  // [N]
+                        : dist_ws + (int64_t)b * N;
+    auto point = [&](int64_t n, float (&q)[CM]) {
+#pragma unroll
+        for (int k = 0; k < CM; ++k) q[k] = (k < C) ? P[n * sn + (int64_t)k * sc] : 0.f;
+    };
+    for (int n = tid; n < N; n += NT) {
+        dist[n] = __float_as_uint(1e10f);
+        if (pts_packed) {
+            float q[CM], sq[CM];
+            point(n, q);
+#pragma unroll
+            for (int k = 0; k < CM; ++k) sq[k] = __fmul_rn(q[k], q[k]);
+            float *dst = pts_packed + ((int64_t)b * N + n) * cp;
+#pragma unroll
+            for (int k = 0; k < CM; ++k)
+                if (k < C) dst[k] = q[k];
+            dst[C] = layout_sum<CM>(sq, C, point_rule(kind, n, N));
+            for (int k = C + 1; k < cp; ++k) dst[k] = 0.f;
+        }
+    }
+    int far = (int)start[b];
+    float c[CM];
+    point(far, c);
+    __syncthreads();
+    int64_t *oi = out_idx + (int64_t)b * S;
+    for (int i = 0;; ++i) {
+        if (tid == 0) oi[i] = far;
+        if (i == S - 1) break;
+        unsigned long long best = 0ull;
+        for (int n = tid; n < N; n += NT) {
+            float q[CM], sq[CM];
+            point(n, q);
+#pragma unroll
+            for (int k = 0; k < CM; ++k) {
+                const float d = q[k] - c[k];
+                sq[k] = __fmul_rn(d, d);
+            }
+            float dd;
+            if constexpr (FIXED && CM == 3) dd = seq_sum<CM>(sq, C);  // every rule agrees for C=3
+            else dd = layout_sum<CM>(sq, C, point_rule(kind, n, N));
+            const unsigned v = min(dist[n], __float_as_uint(dd));  // strict '<' update
+            dist[n] = v;
+            const unsigned long long key = ((unsigned long long)v << 32) | (0xFFFFFFFFu - (unsigned)n);
+            best = key > best ? key : best;
+        }
+        best = wave_max_u64(best);
+        const int par = i & 1;
+        if (lane == 0) slots[par * NW + wave] = best;
+        __syncthreads();  // the other parity's slots were last read before this barrier
+        unsigned long long g = slots[par * NW];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) {
+            const unsigned long long v = slots[par * NW + w];
+            g = v > g ? v : g;
+        }
+        far = (int)(0xFFFFFFFFu - (unsigned)g);
+        point(far, c);
+    }
+    __syncthreads();
+    for (int i = tid; i < S; i += NT) {
+        const int64_t n = __hip_atomic_load(oi + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (out_pts || out_packed) {
+            float q[CM], sq[CM];
+            point(n, q);
+#pragma unroll
+            for (int k = 0; k < CM; ++k) sq[k] = __fmul_rn(q[k], q[k]);
+            if (out_pts) {
+                float *o = out_pts + ((int64_t)b * S + i) * C;
+#pragma unroll
+                for (int k = 0; k < CM; ++k)
+                    if (k < C) o[k] = q[k];
+            }
+            if (out_packed) {
+                float *o = out_packed + ((int64_t)b * S + i) * cp;
+#pragma unroll
+                for (int k = 0; k < CM; ++k)
+                    if (k < C) o[k] = q[k];
+                o[C] = contig_sum<CM>(sq, C);
+                for (int k = C + 1; k < cp; ++k) o[k] = 0.f;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------- pack kernel
 template <int CM>
 __global__ __launch_bounds__(256) void pack_points_kernel(const float *__restrict__ pts, int64_t B,
@@ -400,26 +519,76 @@ static int dispatch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64
     if constexpr (CM > 3)
         if (N <= 16384) return launch_fps<1024, 16, CM, FIXED, 3>(A);
 #undef A
-    return set_error(PN2_EUNSUPPORTED, "pn2_fps_f32: N=%lld exceeds %d points", (long long)N, 16384);
+    return set_error(PN2_EUNSUPPORTED, "pn2_fps_f32: N=%lld: no register-resident shape", (long long)N);
+}
+
+// the register-resident kernels' limits (dispatch_fps); past them the streamed kernel
+static bool fps_resident(int64_t N, int64_t S) { return N <= 16384 && S <= kFpsMaxS; }
+static size_t fps_stream_lds(int64_t N) { return (size_t)2 * (kFpsStreamT / 64) * 8 + (size_t)N * 4; }
+static bool fps_stream_dl(int64_t N) { return fps_stream_lds(N) <= (size_t)160 * 1024; }
+
+template <int CM, bool FIXED>
+static int launch_fps_stream(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+                             int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
+                             float *out_packed, float *pts_packed, unsigned *ws, hipStream_t st) {
+    const int kind = layout_kind(sn, sc);
+    const int cp = (int)pn2_packed_stride(C);
+    if (fps_stream_dl(N)) {
+        static const hipError_t attr = hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&fps_stream_kernel<CM, FIXED, true>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        PN2_REQUIRE(attr == hipSuccess, "pn2_fps_f32: LDS attribute: %s", hipGetErrorString(attr));
+        hipLaunchKernelGGL((fps_stream_kernel<CM, FIXED, true>), dim3((unsigned)B), dim3(kFpsStreamT),
+                           fps_stream_lds(N), st, pts, (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx,
+                           out_pts, out_packed, pts_packed, cp, nullptr);
+    } else {
+        hipLaunchKernelGGL((fps_stream_kernel<CM, FIXED, false>), dim3((unsigned)B), dim3(kFpsStreamT),
+                           fps_stream_lds(0), st, pts, (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx,
+                           out_pts, out_packed, pts_packed, cp, ws);
+    }
+    PN2_LAUNCH_CHECK("fps_stream_kernel");
+    return PN2_OK;
+}
+
+extern "C" int64_t pn2_fps_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t S) {
+    if (B < 0 || N < 1 || C < 1 || S < 1) return -1;
+    return (fps_resident(N, S) || fps_stream_dl(N)) ? 0 : B * N * 4;
+}
+
+extern "C" int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+                              int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
+                              float *out_packed, float *pts_packed, void *workspace, int64_t workspace_bytes,
+                              void *stream) {
+    PN2_REQUIRE(pts && start && out_idx, "pn2_fps_f32: null pointer");
+    PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && S >= 1 && N < INT32_MAX && S < INT32_MAX,
+                "pn2_fps_f32: bad shape B=%lld N=%lld C=%lld S=%lld", (long long)B, (long long)N, (long long)C,
+                (long long)S);
+    PN2_REQUIRE(C <= kMaxC, "pn2_fps_f32: unsupported C=%lld (max %d)", (long long)C, kMaxC);
+    const int64_t need = pn2_fps_workspace_bytes(B, N, C, S);
+    PN2_REQUIRE(workspace_bytes >= need && (need == 0 || workspace),
+                "pn2_fps_f32: N=%lld needs pn2_fps_workspace_bytes = %lld bytes of workspace", (long long)N,
+                (long long)need);
+    if (B == 0) return PN2_OK;
+    hipStream_t st = as_stream(stream);
+#define A pts, B, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed
+    if (!fps_resident(N, S)) {
+        unsigned *ws = reinterpret_cast<unsigned *>(workspace);
+        if (C == 3) return launch_fps_stream<3, true>(A, ws, st);
+        if (C == 10) return launch_fps_stream<10, true>(A, ws, st);
+        return launch_fps_stream<kMaxC, false>(A, ws, st);
+    }
+    if (C == 3) return dispatch_fps<3, true, 16384>(A, st);
+    if (C == 10) return dispatch_fps<10, true, 8192>(A, st);
+    return dispatch_fps<kMaxC, false, 4096>(A, st);
+#undef A
 }
 
 extern "C" int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,
                            int64_t sn, int64_t sc, const int64_t *start, int64_t S,
                            int64_t *out_idx, float *out_pts, float *out_packed, float *pts_packed,
                            void *stream) {
-    PN2_REQUIRE(pts && start && out_idx, "pn2_fps_f32: null pointer");
-    PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && S >= 1, "pn2_fps_f32: bad shape B=%lld N=%lld C=%lld S=%lld",
-                (long long)B, (long long)N, (long long)C, (long long)S);
-    PN2_REQUIRE(S <= kFpsMaxS, "pn2_fps_f32: S=%lld exceeds %d", (long long)S, kFpsMaxS);
-    if (B == 0) return PN2_OK;
-    hipStream_t st = as_stream(stream);
-#define A pts, B, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed, st
-    if (C == 3) return dispatch_fps<3, true, 16384>(A);
-    if (C == 10) return dispatch_fps<10, true, 8192>(A);
-    if (C <= kMaxC) return dispatch_fps<kMaxC, false, 4096>(A);
-#undef A
-    return set_error(PN2_EUNSUPPORTED, "pn2_fps_f32: unsupported C=%lld (max %d)", (long long)C,
-                     kMaxC);
+    return pn2_fps_ws_f32(pts, B, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed, nullptr, 0,
+                          stream);
 }
 
 extern "C" int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,

@@ -66,6 +66,9 @@ SIGNATURES = {
     "pn2_last_error": (ctypes.c_char_p, []),
     "pn2_packed_stride": (_i64, [_i64]),
     "pn2_fps_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "pn2_fps_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
+    "pn2_fps_ws_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
+                              _i64, _vp]),
     "pn2_pack_points_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pn2_ball_query_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp]),
     "pn2_ball_query_cnt_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp, _vp]),
@@ -111,7 +114,7 @@ SIGNATURES = {
                                _int, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 _lib = None
 
 

@@ -135,9 +135,14 @@ def fps_direct(points: Tensor, npoint: int, start: Tensor) -> Tuple[Tensor, Tens
     cpk = torch.empty(B, npoint, cp, dtype=torch.float32, device=points.device)
     ppk = torch.empty(B, N, cp, dtype=torch.float32, device=points.device)
     sb, sn, sc = points.stride()
-    _run("pn2_fps_f32", _L.pn2_fps_f32,
+    # past the register-resident shapes (N > 16384, npoint > 8192) the streamed kernel; past
+    # N = 40952 it keeps the running distances in this workspace
+    nws = int(_L.pn2_fps_workspace_bytes(B, N, C, npoint))
+    ws = torch.empty(max(nws, 0) // 4, dtype=torch.float32, device=points.device) if nws > 0 else None
+    _run("pn2_fps_f32", _L.pn2_fps_ws_f32,
          (points.data_ptr(), B, N, C, sb, sn, sc, start.data_ptr(), npoint, idx.data_ptr(),
-          newp.data_ptr(), cpk.data_ptr(), ppk.data_ptr(), _stream(points)), points.device,
+          newp.data_ptr(), cpk.data_ptr(), ppk.data_ptr(), 0 if ws is None else ws.data_ptr(),
+          max(nws, 0), _stream(points)), points.device,
          flops=float(B) * npoint * N * (3 * C + 2))
     return idx, newp, cpk, ppk
 
@@ -441,10 +446,20 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
     ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=dev_t.device) if ws_bytes else None
     M = B * S * K
     flops = 2.0 * M * sum(cins[i] * wts[i].shape[1] for i in range(n))  # algorithmic, cin unpadded
+    # compulsory bytes: every source element, index and weight read once, the output written once
+    if mode == _lib.SRC_ROWS:
+        nbytes = 4.0 * B * K * cins[0]
+    else:
+        nbytes = 4.0 * B * N * (C + D)
+        if mode != _lib.SRC_GROUP_ALL:
+            nbytes += 4.0 * B * S * C + 8.0 * B * S * K + (4.0 * B * S if cnt is not None else 0.0)
+    nbytes += sum(4.0 * (cins[i] + 2) * wts[i].shape[1] for i in range(n))
+    nbytes += 4.0 * (B * S if pool else M) * wts[-1].shape[1]
     name = "pn2_sa_mlp_max_bf16" if bf16 else "pn2_sa_mlp_max_f32"
     _run(name, getattr(_L, name),
          (src, layers, n, 1 if pool else 0, out.data_ptr(), out.stride(-2),
-          0 if ws is None else ws.data_ptr(), ws_bytes, _stream(dev_t)), dev_t.device, flops=flops)
+          0 if ws is None else ws.data_ptr(), ws_bytes, _stream(dev_t)), dev_t.device, flops=flops,
+         nbytes=nbytes)
 
 
 sa_mlp_max_ = torch.library.custom_op("pn2::sa_mlp_max_", sa_mlp_max_direct, mutates_args=("out", "zero"))

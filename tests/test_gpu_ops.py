@@ -167,6 +167,37 @@ def test_fps_stress_size_vs_oracle():
         np.testing.assert_array_equal(idx.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("kind,layout,N,S", [
+    ("uniform3", "strided", 32768, 512),  # streamed kernel, running distances in LDS
+    ("uniform3", "contig", 50000, 256),   # streamed, distances in the caller workspace
+    ("onehot10", "strided", 20000, 256),  # 10 channels past the resident cap
+    ("random13", "contig", 17000, 128),   # the generic-C kernel
+    ("randn10", "contig", 18000, 128),    # 10 varying channels: the channel-sum order
+    ("dup3", "strided", 20000, 256),      # many exact duplicates: first-index ties
+    ("uniform3", "contig", 9000, 8500),   # npoint past the resident 8192
+])
+def test_fps_streamed_past_resident_caps(kind, layout, N, S):
+    """The shapes past the register-resident kernels (N > 16384, npoint > 8192) run the
+    streamed FPS: indices bit-exact vs the oracle (pointnet2_utils.py:47-68), the gathered
+    centroids and the packed records feed the same ball query."""
+    B = 2
+    if kind == "random13":
+        p = torch.randn(B, N, 13, generator=torch.Generator().manual_seed(N)) * 0.5
+    else:
+        p = cases.cloud(kind, B, N, 4)
+    p = cases.as_layout(p, layout)
+    start = torch.tensor([7, N - 2])
+    want = oracle.farthest_point_sample(p, S, start)
+    dp = _to_dev_view(p)
+    idx, newp, cpk, ppk = torch.ops.pn2.fps(dp, S, start.to(DEV))
+    np.testing.assert_array_equal(idx.cpu().numpy(), want)
+    ctr = oracle.index_points(p, want)
+    np.testing.assert_array_equal(newp.cpu().numpy(), ctr)
+    C = p.shape[2]
+    exp = oracle.query_ball_point(0.2, 16, p, ctr)
+    np.testing.assert_array_equal(torch.ops.pn2.ball_query(ppk, cpk, C, 0.2, 16).cpu().numpy(), exp)
+
+
 def test_no_neighbour_centroids_flagged_not_read_out_of_bounds():
     """Clouds on a millimetre scale: the -2ab + a^2 + b^2 cancellation puts some centroids'
     distance to themselves above a small r^2, so they have no neighbour.  The reference pads

@@ -25,7 +25,7 @@ FORWARD_MARKER = "fps_kernel"  # one launch per sampled SA layer, counted below
 # kernels one pn2_sa_mlp_max_f32 call may dispatch
 MLP_KERNELS = ("sa_mlp_kernel", "dense_layer_kernel", "sa_chain_kernel", "dense_split_kernel",
                "dense_lds_kernel", "compact_scan_kernel", "u_table_kernel", "unkey_kernel")
-FPS_PER_FORWARD = {"ssg": 2, "msg": 2, "pose": 4, "stress": 2}
+FPS_PER_FORWARD = {"ssg": 2, "msg": 2, "pose": 3, "stress": 2}
 # pn2_ball_query_f32 calls per forward (one per radius of every grouping SA layer)
 BQ_PER_FORWARD = {"ssg": 2, "msg": 6, "pose": 3, "stress": 2}
 # the MLP entry point each config's bench line names (config 5 runs the bf16 MLP)
