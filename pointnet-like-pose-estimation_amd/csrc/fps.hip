@@ -11,9 +11,11 @@
 // level plus a ballot, no second (index) reduction.  One iteration:
 //   branchless distance of every owned point to the centroid in the reference's exact float32
 //   order (differences, exact squares, layout-dependent channel sum, no FMA contraction) ->
-//   strict-< min update -> per-lane first-argmax (v_cndmask, no exec branches) -> wave max by DPP
-//   + ballot/ctz for the owner lane -> [NW > 1] the owner writes {max, index, coordinates} to its
-//   wave's LDS slot (double-buffered by iteration parity), ONE barrier, every wave reads all NW
+//   strict-< min update -> per-lane max -> wave max by DPP + ballot/ctz for the owner lane -> the
+//   owner's first point at the max by one ballot per point (wave-uniform index, SALU scan) and its
+//   coordinates by one indexed register move each -> [NW > 1] the owner writes {max, index,
+//   coordinates} to its wave's LDS slot (double-buffered by iteration parity), ONE barrier,
+//   every wave reads all NW
 //   slots (one lane each), DPP max over a 16-lane row + ballot picks the winning wave and
 //   v_readlane broadcasts its index/coordinates.  No second barrier, no global memory in the loop.
 // The sampled indices are kept in LDS and written, with the gathered centroids and the packed
@@ -83,13 +85,17 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
     constexpr int PH = (PPT + 1) / 2;
     static_assert(CR == CM || (CR <= 3 && !LDSC), "partial register residency: xyz or nothing");
     constexpr int CQ = CR > 0 ? CR : 1;
-    pn2_f2 q[PH][CQ];
+    // per channel, the owned points' coordinates as one register vector: pairs feed the packed
+    // distance ops, and a wave-uniform index selects one element with a single indexed move
+    // (s_set_gpr_idx) instead of a select chain
+    typedef float VQ __attribute__((ext_vector_type(2 * PH)));
+    VQ q[CQ];
     unsigned dist[PPT];
     // channel k of owned point j: registers, or the input (through `base`, which the serial
     // loop launders every iteration so the compiler cannot hoist the re-reads out of it into
     // registers the kernel does not have)
     auto coord = [&](const float *base, int j, int k) -> float {
-        if (k < CR) return q[j >> 1][k < CQ ? k : 0][j & 1];
+        if (k < CR) return q[k < CQ ? k : 0][j];
         const int n = tid * PPT + j;
         return (j < PPT && n < N && k < C) ? base[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
     };
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
 #pragma unroll
         for (int k = 0; k < CM; ++k) {
             pj[k] = (valid && k < C) ? P[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
-            if (k < CR) q[j >> 1][k < CQ ? k : 0][j & 1] = pj[k];
+            if (k < CR) q[k < CQ ? k : 0][j] = pj[k];
         }
         if (j < PPT) dist[j] = valid ? __float_as_uint(1e10f) : 0u;
         if ((j & 1) == 0) rule[j >> 1] = point_rule(kind, n, N);
@@ -175,7 +181,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
                 pn2_f2 s3[3];
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    const pn2_f2 qk = k < CR ? q[h][k < CQ ? k : 0]
+                    const pn2_f2 qk = k < CR ? pn2_f2{q[k < CQ ? k : 0][2 * h], q[k < CQ ? k : 0][2 * h + 1]}
                                              : pn2_f2{coord(Pl, 2 * h, k), coord(Pl, 2 * h + 1, k)};
                     const pn2_f2 d = qk - c[k];
                     s3[k] = d * d;
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
                 pn2_f2 sq[CM];
 #pragma unroll
                 for (int k = 0; k < CM; ++k) {
-                    const pn2_f2 qk = k < CR ? q[h][k < CQ ? k : 0]
+                    const pn2_f2 qk = k < CR ? pn2_f2{q[k < CQ ? k : 0][2 * h], q[k < CQ ? k : 0][2 * h + 1]}
                                              : pn2_f2{coord(Pl, 2 * h, k), coord(Pl, 2 * h + 1, k)};
                     const pn2_f2 d = qk - c[k];
                     sq[k] = d * d;
@@ -203,12 +209,15 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
         // wave: max value, then its first lane (contiguous ownership -> smallest index)
         const unsigned wv = wave_max_u32(bv);
         const int ol = (int)__builtin_ctzll(__ballot(bv == wv));
-        int bj = PPT - 1;  // first owned point holding the lane's max
+        // the owner lane's first point holding the max, wave-uniform: one compare per point
+        // writes its lane mask straight to an SGPR pair, the scan over the owner's bit is SALU
+        int bj = PPT - 1;
 #pragma unroll
-        for (int j = PPT - 2; j >= 0; --j) bj = (dist[j] == bv) ? j : bj;
+        for (int j = PPT - 2; j >= 0; --j)
+            if ((__ballot(dist[j] == wv) >> ol) & 1ull) bj = j;
         if constexpr (LDSC) {
             if constexpr (NW == 1) {
-                far = ol * PPT + __builtin_amdgcn_readlane(bj, ol);
+                far = ol * PPT + bj;
             } else {
                 // one 64-bit LDS max per wave: key = dist bits : ~index (max dist, then first
                 // index).  key[i%3] is reset one iteration ahead; its last reader passed the
@@ -228,10 +237,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
 #pragma unroll
             for (int k = 0; k < CM; ++k) {
                 if (k < CR) {
-                    float v = q[0][k < CQ ? k : 0].x;
-#pragma unroll
-                    for (int j = 1; j < PPT; ++j) v = (bj == j) ? q[j >> 1][k < CQ ? k : 0][j & 1] : v;
-                    bc[k] = v;
+                    bc[k] = q[k < CQ ? k : 0][bj];  // meaningful in the owner lane
                 } else if (k < 3 || !xyz_only) {  // the owner lane reads its point's other channels
                     const int n = tid * PPT + bj;
                     bc[k] = (lane == ol && n < N && k < C) ? Pl[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
                 }
             }
             if constexpr (NW == 1) {
-                far = ol * PPT + __builtin_amdgcn_readlane(bj, ol);
+                far = ol * PPT + bj;
 #pragma unroll
                 for (int k = 0; k < CM; ++k)
                     c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bc[k]), ol));
@@ -501,6 +507,9 @@ static int dispatch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64
     if (fnt == nt && fppt == ppt && N <= (int64_t)nt * ppt) return launch_fps<nt, ppt, CM, FIXED>(A);
     PN2_FPS_TRY(64, 8) PN2_FPS_TRY(64, 16) PN2_FPS_TRY(128, 4) PN2_FPS_TRY(128, 8) PN2_FPS_TRY(256, 2)
     PN2_FPS_TRY(256, 4) PN2_FPS_TRY(512, 2) PN2_FPS_TRY(1024, 1) PN2_FPS_TRY(512, 4) PN2_FPS_TRY(1024, 2)
+    if constexpr (CM == 3) {
+        PN2_FPS_TRY(512, 16) PN2_FPS_TRY(512, 32) PN2_FPS_TRY(256, 32) PN2_FPS_TRY(1024, 8)
+    }
 #undef PN2_FPS_TRY
     if (N <= 256) return launch_fps<64, 4, CM, FIXED>(A);
     // measured on MI355X (tools/bench_fps.py): two points per lane and 4-16 waves win until
@@ -563,7 +572,7 @@ extern "C" int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C,
     PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && S >= 1 && N < INT32_MAX && S < INT32_MAX,
                 "pn2_fps_f32: bad shape B=%lld N=%lld C=%lld S=%lld", (long long)B, (long long)N, (long long)C,
                 (long long)S);
-    PN2_REQUIRE(C <= kMaxC, "pn2_fps_f32: unsupported C=%lld (max %d)", (long long)C, kMaxC);
+    if (C > kMaxC) return set_error(PN2_EUNSUPPORTED, "pn2_fps_f32: unsupported C=%lld (max %d)", (long long)C, kMaxC);
     const int64_t need = pn2_fps_workspace_bytes(B, N, C, S);
     PN2_REQUIRE(workspace_bytes >= need && (need == 0 || workspace),
                 "pn2_fps_f32: N=%lld needs pn2_fps_workspace_bytes = %lld bytes of workspace", (long long)N,

@@ -1,6 +1,8 @@
-"""Sweep the FPS kernel's block shapes (PN2_FPS_CFG) on the GPU for the BASELINE geometries,
-checking every variant against the CPU oracle first.  Prints one line per (shape, variant):
-microseconds per launch and per serial iteration."""
+"""Sweep the FPS kernel's block shapes (tuning keys fps_threads / fps_ppt) on the GPU for the
+BASELINE geometries, checking every variant against the CPU oracle first.  Prints one line per
+(shape, variant): microseconds per launch and per serial iteration.
+    python tools/bench_fps.py [--default-only] [--tag NAME]
+(PN2_TUNING=lib=<path> times another build of the library.)"""
 import json
 import os
 import sys
@@ -28,7 +30,10 @@ VARIANTS = ["64x4", "64x8", "64x16", "128x4", "128x8", "256x2", "256x4", "512x2"
 
 
 def main():
+    from pn2 import tuning
     dev = torch.device("cuda")
+    only_default = "--default-only" in sys.argv
+    tag = sys.argv[sys.argv.index("--tag") + 1] if "--tag" in sys.argv else ""
     res = []
     for name, B, N, C, S, kind in SHAPES:
         x = cases.as_layout(cases.cloud(kind, B, N, 5), "strided")
@@ -36,31 +41,28 @@ def main():
         start = torch.randint(0, N, (B,), generator=torch.Generator().manual_seed(1))
         sd = start.to(dev)
         want = oracle.farthest_point_sample(x[:2], S, start[:2])
-        for v in VARIANTS:
-            if v:
-                nt, ppt = map(int, v.split("x"))
-                if nt * ppt < N or nt * ppt >= 4 * N:
-                    continue
-            os.environ["PN2_FPS_CFG"] = v
-            try:
-                idx = torch.ops.pn2.fps(xd, S, sd)[0]
-            except Exception as e:  # variant not compiled for this C
+        only = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--variants=")]
+        for v in (only[0] if only else [""] if only_default else VARIANTS):
+            nt, ppt = map(int, v.split("x")) if v else (0, 0)
+            if v and (nt * ppt < N or (nt * ppt >= 4 * N and not only)):
                 continue
-            ok = bool((idx[:2].cpu().numpy() == want).all())
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            reps = 5
-            e0.record()
-            for _ in range(reps):
-                torch.ops.pn2.fps(xd, S, sd)
-            e1.record()
-            torch.cuda.synchronize()
+            with tuning.override(fps_threads=nt, fps_ppt=ppt):
+                idx = torch.ops.pn2.fps(xd, S, sd)[0]
+                ok = bool((idx[:2].cpu().numpy() == want).all())
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                reps = 5
+                e0.record()
+                for _ in range(reps):
+                    torch.ops.pn2.fps(xd, S, sd)
+                e1.record()
+                torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / reps
-            r = {"shape": name, "variant": v or "default", "us": round(us, 1), "us_per_iter": round(us / S, 3), "exact": ok}
+            r = {"tag": tag, "shape": name, "variant": v or "default", "us": round(us, 1),
+                 "us_per_iter": round(us / S, 3), "exact": ok}
             print(json.dumps(r), flush=True)
             res.append(r)
-    os.environ.pop("PN2_FPS_CFG", None)
-    with open(os.path.join(ROOT, "gpurun_out", "fps_sweep.json"), "w") as fh:
+    with open(os.path.join(ROOT, "gpurun_out", "fps_sweep%s.json" % ("_" + tag if tag else "")), "w") as fh:
         json.dump(res, fh, indent=1)
 
 
