@@ -108,6 +108,14 @@ def parse():
                     help="shared-MLP arithmetic (default: bf16 for --config stress, else fp32)")
     ap.add_argument("--geometry-cus", type=int, default=0,
                     help="CUs reserved for the FPS chain (0: streams share every CU)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
+    ap.add_argument("--gather-every", type=int, default=8,
+                    help="pipelined runs: all_gather the head outputs of this many batches in "
+                         "one collective (1: one collective per batch)")
+    ap.add_argument("--force-rccl", action="store_true",
+                    help="run the per-step all_gather of the head outputs through RCCL even on "
+                         "one GPU (a 1-rank group): measures the collective's cost")
     ap.add_argument("--plumbing-check", action="store_true",
                     help="no GPU work: ranks join a gloo group, all_gather their shard ranges "
                          "and rank 0 prints a JSON line with n_gpus (tests the launcher on CPU)")
@@ -319,16 +327,34 @@ def main():
                  % (a.gpus, env_world, env_world))
     if a.plumbing_check:
         return plumbing_check(a)
+    if a.hw_queues > 0:
+        # HW queues per process (read by the HIP runtime at its first call, below).  The
+        # pipeline keeps 4 streams busy (caller, geometry, compute, head tail); RCCL adds its own
+        # streams, and with HIP's default of 4 queues two of the pipeline's streams then share
+        # one: -10 % at world size 1 with the all_gather forced through RCCL (115 vs 129-131k),
+        # nothing with 8 queues (131k); no change without RCCL
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or a.force_rccl:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if world == 1:  # --force-rccl: a 1-rank RCCL group of its own
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     import pn2  # noqa: F401
-    from pn2 import ops, shard
+    from pn2 import ops, shard, tuning
+    if a.force_rccl:
+        # every step's all_gather of the head outputs runs through RCCL at world size 1 (the
+        # collective's queue and launch cost on one GPU)
+        tuning.override(force_gather=1).__enter__()
+    if os.environ.get("PN2_BENCH_AFFINITY"):  # diagnostics: the host threads' CPU affinity
+        print("affinity before first collective:", len(os.sched_getaffinity(0)), file=sys.stderr)
 
     head, B, N, kind, desc = CONFIGS[a.config]
     prec = a.precision or DEFAULT_PRECISION.get(a.config, "fp32")
@@ -376,15 +402,29 @@ def main():
                     for h in o]
         return shard.all_gather_rows(o[0] if isinstance(o, tuple) else o, sizes="shard")
 
+    def first_outputs(o):  # every head's first output (the logits / predictions)
+        if len(names) > 1:
+            return [h[0] if isinstance(h, tuple) else h for h in o]
+        return o[0] if isinstance(o, tuple) else o
+
     def run_pipelined(k):
         with shard.batch_shard(gB, lo):
-            pf.run([x] * k, [(mean,)] * k if takes_mean else None, post=gather)
+            if a.gather_every > 1:  # one collective per gather_every batches
+                bg = shard.BatchedGather(a.gather_every, total=k)
+                post = lambda i, o: bg(i, first_outputs(o))  # noqa: E731
+            else:
+                post = gather
+            pf.run([x] * k, [(mean,)] * k if takes_mean else None, post=post)
 
     for _ in range(max(a.warmup, 2) if a.graph else a.warmup):  # graph: 1st call captures
         step(names, models, x, mean, gB, lo)
     if pipelined:
         run_pipelined(max(a.warmup, 2))
     torch.cuda.synchronize()
+    if os.environ.get("PN2_BENCH_AFFINITY"):
+        import threading
+        print("affinity after warmup:", len(os.sched_getaffinity(0)), "threads:",
+              threading.active_count(), "os threads:", len(os.listdir("/proc/self/task")), file=sys.stderr)
 
     def timed(k, timer, models=models, pipe=False):
         if world > 1:
@@ -487,7 +527,8 @@ def main():
                     "random-init weights and BN statistics (eval mode)" % (
                         " + 7-way one-hot" if kind == "onehot10" else ""),
             "config": {"workload": desc, "global_batch": gB, "points": N, "heads": names,
-                       "parallelism": "dp%d" % world},
+                       "parallelism": "dp%d" % world + (" (all_gather forced through RCCL)"
+                                                         if a.force_rccl else "")},
             "roofline": roof, "roofline_ball_query": roof_bq, "cpu_baseline": cpu, "kernels": kernels,
             "launch": ("hip_graph" if a.graph else
                        "%s pipeline (fps%s stream%s)" % (

@@ -18,6 +18,8 @@ import threading
 import torch
 import torch.distributed as dist
 
+from . import tuning
+
 _state = threading.local()
 
 
@@ -94,7 +96,7 @@ def all_gather_rows(local, group=None, sizes=None):
     if not dist.is_available() or not dist.is_initialized():
         return local
     world = dist.get_world_size(group)
-    if world == 1:
+    if world == 1 and not tuning.get("force_gather"):
         return local
     local = local.contiguous()
     if isinstance(sizes, str):
@@ -127,3 +129,40 @@ def all_gather_rows(local, group=None, sizes=None):
     if all(n == m for n in sizes):
         return out
     return torch.cat([out[r * m:r * m + n] for r, n in enumerate(sizes)])
+
+
+class BatchedGather:
+    """A pipeline ``post`` callback that gathers the heads' per-batch outputs across the ranks
+    in one collective per `every` batches instead of one per batch: the outputs of the batches
+    since the last gather are stacked along a new dim 1 ([b_r, n, ...] per head), all-gathered
+    by rows (``all_gather_rows``) and split back, so ``results`` holds, per batch, exactly what
+    a per-batch ``all_gather_rows`` returns.  Every rank must see the same call sequence.
+    `total` (the batch count) flushes the last partial bundle; ``flush()`` does it otherwise.
+    (One RCCL collective per batch costs ~10 % of the pipelined SSG rate even on one GPU --
+    DESIGN.md §6; batching the exchange keeps the queues to the pipeline's own.)"""
+
+    def __init__(self, every, total=None, sizes="shard"):
+        self.every, self.total, self.sizes = max(1, int(every)), total, sizes
+        self.pending, self.results, self.calls = [], [], 0
+
+    def __call__(self, i, out):
+        heads = list(out) if isinstance(out, (tuple, list)) else [out]
+        self.pending.append(heads)
+        self.calls += 1
+        if len(self.pending) == self.every or (self.total is not None and self.calls == self.total):
+            self.flush()
+        return out
+
+    def flush(self):
+        if not self.pending:
+            return
+        n = len(self.pending)
+        per_head = []
+        for h in range(len(self.pending[0])):
+            local = torch.stack([p[h] for p in self.pending], 1)
+            g = all_gather_rows(local, sizes=self.sizes)
+            per_head.append([g[:, j] for j in range(n)])
+        for j in range(n):
+            hs = [ph[j] for ph in per_head]
+            self.results.append(hs if len(hs) > 1 else hs[0])
+        self.pending = []

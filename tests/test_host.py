@@ -144,6 +144,51 @@ def test_gloo_all_gather_and_rng_parity(B, world):
         np.testing.assert_array_equal(got[:, 1], owner)
 
 
+def _batched_gather_worker(rank, world, port, out, B, every):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, PKG)
+    from pn2 import shard
+    lo, hi = shard.shard_range(B, rank, world)
+    nb = 5
+    # per batch i: two "heads" of different widths, rows tagged by cloud and batch
+    outs = [[torch.arange(lo, hi, dtype=torch.float64)[:, None] * 10 + i + torch.zeros(1, 3, dtype=torch.float64),
+             torch.full((hi - lo, 2), float(rank * 100 + i), dtype=torch.float64)] for i in range(nb)]
+    with shard.batch_shard(B, lo):
+        bg = shard.BatchedGather(every, total=nb)
+        for i, o in enumerate(outs):
+            bg(i, o)
+        want = [[shard.all_gather_rows(h, sizes="shard") for h in o] for o in outs]
+    if rank == 0:
+        out.put(([[h.numpy() for h in r] for r in bg.results], [[h.numpy() for h in r] for r in want]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B,world,every", [(8, 2, 2), (7, 3, 4), (7, 2, 1)])
+def test_batched_gather_matches_per_batch(B, world, every):
+    """shard.BatchedGather (the pipelined bench's exchange: one collective per `every` batches)
+    returns, per batch, exactly what a per-batch all_gather_rows returns -- uneven shards, two
+    heads, and a last partial bundle (5 batches)."""
+    import random
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    procs = [ctx.Process(target=_batched_gather_worker, args=(r, world, port, q, B, every))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got, want = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(got) == len(want) == 5
+    for g, w in zip(got, want):
+        for gh, wh in zip(g, w):
+            np.testing.assert_array_equal(gh, wh)
+
+
 BENCH = os.path.join(os.path.dirname(PKG), "bench.py")
 
 
