@@ -58,7 +58,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 11
+#define PN2_ABI_VERSION 12
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -131,6 +131,11 @@ int pn2_ball_query_f32(const float *pts_packed, const float *ctr_packed, int64_t
 int pn2_ball_query_cnt_f32(const float *pts_packed, const float *ctr_packed, int64_t B,
                            int64_t N, int64_t S, int64_t C, double radius, int64_t K,
                            int64_t *out_idx, int32_t *out_cnt, void *stream);
+/* The same lists as int32 (half the bytes; the SA layers' fused path reads them through
+ * pn2_sa_src.idx32).  Entries, padding and counts as pn2_ball_query_cnt_f32. */
+int pn2_ball_query_i32(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N,
+                       int64_t S, int64_t C, double radius, int64_t K, int32_t *out_idx,
+                       int32_t *out_cnt, void *stream);
 
 /* square_distance(src, dst) -> out [B,S,N] float32 from packed records of src [B,S,cp] and
  * dst [B,N,cp] (same float32 recipe as the ball query). */
@@ -220,6 +225,8 @@ typedef struct pn2_sa_src {
                                              (group_all's new_points, the reference's
                                              torch.zeros(B,1,C), pointnet2_utils.py:136),
                                              done by one of the call's launches          */
+    const int32_t *idx32;                 /* [B,S,K] int32 (pn2_ball_query_i32), read in
+                                             place of idx when not NULL (group modes)    */
 } pn2_sa_src;
 
 /* Bytes of workspace pn2_sa_mlp_max_f32 needs for this layer chain: 0 when the chain runs as

@@ -57,10 +57,9 @@ int read_bq_errors(unsigned *bits, int clear) {
 // CC > 0: the channel count is known at compile time (C = 3 xyz, C = 10 pose) and the shape is
 // not ATen's naive-bmm size; CC = 0: runtime C and the `small` flag.  NW bitmask words per
 // segment (TS = 32*NW points per wave per round).
-// one point record against one centroid: the reference's distance and masking test
+// one point record against one centroid: the reference's distance, then its masking test
 template <int CP>
-__device__ __forceinline__ unsigned bq_near(const float (&c)[CP], float ssq_c, const float *p, int C,
-                                            bool small, float r2) {
+__device__ __forceinline__ float bq_dist(const float (&c)[CP], float ssq_c, const float *p, int C, bool small) {
     float mm = __fmul_rn(c[0], p[0]);
 #pragma unroll
     for (int k = 1; k < CP - 1; ++k)
@@ -69,21 +68,39 @@ __device__ __forceinline__ unsigned bq_near(const float (&c)[CP], float ssq_c, c
 #pragma unroll
     for (int k = 1; k < CP - 1; ++k)
         if (k == C) sp = p[k];  // static register indices (no scratch)
-    const float d = __fadd_rn(__fadd_rn(__fmul_rn(-2.0f, mm), ssq_c), sp);
-    return !(d > r2);
+    // (-2 * mm) is exact, so one fma rounds (-2 * mm) + ssq_c exactly as the separate ops do
+    return __fadd_rn(__builtin_fmaf(-2.0f, mm, ssq_c), sp);
 }
 
-template <int CP, int CC, int NW, int P>
+template <int CP>
+__device__ __forceinline__ unsigned bq_near(const float (&c)[CP], float ssq_c, const float *p, int C,
+                                            bool small, float r2) {
+    return !(bq_dist<CP>(c, ssq_c, p, C, small) > r2);
+}
+
+// wd = 2 wd + hit, hit = !(d > r2) = !(r2 < d): the compare into VCC and one add with carry-in
+// (the compiler's select + shift + or is three instructions)
+__device__ __forceinline__ void bq_insert(unsigned &wd, float d, float r2) {
+    asm volatile("v_cmp_nlt_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(wd) : "s"(r2), "v"(d) : "vcc");
+}
+
+// OT: the index type written (int64: the reference's query_ball_point; int32: the SA path's
+// lists, half the bytes).  Each lane's hits go to its centroid's row of an LDS buffer
+// (64 rows of K + 1 entries, dynamic LDS); after the scan every row is written out whole,
+// padding included, one coalesced row per wave step.
+template <int CP, int CC, int NW, int P, typename OT>
 __global__ __launch_bounds__(64 * P) void ball_query_kernel(
     const float *__restrict__ pts, const float *__restrict__ ctr, int N, int S, int C_, float r2,
-    int K, int small_, int64_t *__restrict__ out, int *__restrict__ out_cnt) {
+    int K, int small_, OT *__restrict__ out, int *__restrict__ out_cnt) {
     constexpr int TS = 32 * NW;
     constexpr int TV = P * TS * CP / 4;  // float4 per staged round
     __shared__ float4 tile[TV];
     const int C = CC > 0 ? CC : C_;
     const bool small = CC > 0 ? false : small_;  // the specialised instances never see tiny shapes
     __shared__ int cnts[2][P][64];
-    __shared__ int firsts[64];
+    extern __shared__ __attribute__((aligned(16))) char bq_dyn[];
+    OT *obuf = reinterpret_cast<OT *>(bq_dyn);  // [64][K + 1]
+    const int KP = K + 1;
 
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -110,7 +127,16 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
 #pragma unroll
     for (int k = 1; k < CP - 1; ++k)
         if (k == C) ssq_c = c[k];  // static register indices (no scratch)
-    if (w == 0) firsts[lane] = N;
+
+    // point i of the staged round as a record
+    auto point_rec = [&](int i, float (&pv)[CP]) {
+        const float4 *tp = tile + i * (CP / 4);
+#pragma unroll
+        for (int v = 0; v < CP / 4; ++v) {
+            const float4 q4 = tp[v];
+            pv[4 * v] = q4.x; pv[4 * v + 1] = q4.y; pv[4 * v + 2] = q4.z; pv[4 * v + 3] = q4.w;
+        }
+    };
 
     int total = valid ? 0 : K;  // hits so far (invalid lanes count as done)
     int r = 0;
@@ -120,8 +146,9 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
         int mine = 0;
         {  // stage the round's P*TS records (coalesced 16-byte loads by the whole workgroup)
             if (R0 > 0) __syncthreads();  // every wave is done with the previous round's tile
-            const int nv = min(P * TS, N - R0) * (CP / 4);
+            const int npt = min(P * TS, N - R0);
             const float4 *src = reinterpret_cast<const float4 *>(pts + ((int64_t)b * N + R0) * CP);
+            const int nv = npt * (CP / 4);
             for (int x = threadIdx.x; x < nv; x += 64 * P) tile[x] = src[x];
             __syncthreads();
         }
@@ -140,19 +167,14 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
                         const float4 q4 = tp[v];
                         pv[4 * v] = q4.x; pv[4 * v + 1] = q4.y; pv[4 * v + 2] = q4.z; pv[4 * v + 3] = q4.w;
                     }
-                    wd = (wd << 1) | bq_near<CP>(c, ssq_c, pv, C, small, r2);  // point base+i -> bit 31-i
+                    bq_insert(wd, bq_dist<CP>(c, ssq_c, pv, C, small), r2);  // point base+i -> bit 31-i
                 }
             } else if (np > 0) {
                 for (int i = 0; i < 32; ++i) {
                     unsigned h = 0;
                     if (i < np) {
-                        const float4 *tp = tile + (w * TS + 32 * t + i) * (CP / 4);
                         float pv[CP];
-#pragma unroll
-                        for (int v = 0; v < CP / 4; ++v) {
-                            const float4 q4 = tp[v];
-                            pv[4 * v] = q4.x; pv[4 * v + 1] = q4.y; pv[4 * v + 2] = q4.z; pv[4 * v + 3] = q4.w;
-                        }
+                        point_rec(w * TS + 32 * t + i, pv);
                         h = bq_near<CP>(c, ssq_c, pv, C, small, r2);
                     }
                     wd = (wd << 1) | h;
@@ -177,8 +199,7 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
             while (wd != 0 && off < K) {
                 const int i = __builtin_clz(wd);
                 const int n = seg0 + 32 * t + i;
-                if (off == 0) firsts[lane] = n;
-                out[q * K + off] = n;
+                obuf[lane * KP + off] = (OT)n;
                 ++off;
                 wd ^= 0x80000000u >> i;
             }
@@ -186,16 +207,17 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
         total += round;
         if (__builtin_amdgcn_ballot_w64(total < K) == 0) break;  // same in every wave
     }
-    __syncthreads();  // firsts[] complete
+    __syncthreads();  // every row's hits are in obuf
 
-    // padding + counts, one centroid row per step (coalesced over the K slots)
+    // rows out, hits then padding (the first hit; N when there is none: the reference's
+    // pad), one centroid row per step, coalesced over the K slots; and the counts
     for (int j = w; j < 64; j += P) {
         if (g0 + j >= S) break;
         const int cj = min(__builtin_amdgcn_readlane(total, j), K);
-        const int fj = firsts[j];
+        const OT fj = cj > 0 ? obuf[j * KP] : (OT)N;
         if (cj == 0 && lane == 0) atomicOr(&g_bq_errors, (unsigned)PN2_DEVERR_NO_NEIGHBOUR);
-        int64_t *o = out + ((int64_t)b * S + g0 + j) * K;
-        for (int k = cj + lane; k < K; k += 64) o[k] = fj;
+        OT *o = out + ((int64_t)b * S + g0 + j) * K;
+        for (int k = lane; k < K; k += 64) o[k] = k < cj ? obuf[j * KP + k] : fj;
         if (out_cnt && lane == 0) out_cnt[(int64_t)b * S + g0 + j] = cj;
     }
 }
@@ -204,9 +226,9 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
 
 using namespace pn2;
 
-template <int CP, int CC>
+template <int CP, int CC, typename OT>
 static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, int64_t S,
-                     int64_t C, float r2, int64_t K, int64_t *out, int *cnt, hipStream_t st) {
+                     int64_t C, float r2, int64_t K, OT *out, int *cnt, hipStream_t st) {
     const int64_t nblk = B * ((S + 63) / 64);
     PN2_REQUIRE(nblk < (int64_t)1 << 31, "pn2_ball_query_f32: too many centroids");
     // waves per workgroup: 16 for long xyz clouds (more segments in flight), else 8
@@ -218,9 +240,17 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
     int nw = per_wave <= 32 ? 1 : per_wave <= 64 ? 2 : 4;
     if (CP > 4 && nw > 2) nw = 2;
     const int sm = (int)(S * N * C < 400);
-#define PN2_BQ_L(NW, PP)                                                                     \
-    hipLaunchKernelGGL((ball_query_kernel<CP, CC, NW, PP>), dim3((unsigned)nblk), dim3(64 * PP), \
-                       0, st, pp, cp_, (int)N, (int)S, (int)C, r2, (int)K, sm, out, cnt)
+    const size_t obytes = (size_t)64 * (K + 1) * sizeof(OT);
+    PN2_REQUIRE(obytes <= 96 * 1024, "pn2_ball_query_f32: K=%lld too large", (long long)K);
+#define PN2_BQ_L(NW, PP)                                                                               \
+    do {                                                                                               \
+        static const hipError_t attr = hipFuncSetAttribute(                                           \
+            reinterpret_cast<const void *>(&ball_query_kernel<CP, CC, NW, PP, OT>),                   \
+            hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);                                   \
+        PN2_REQUIRE(attr == hipSuccess, "pn2_ball_query_f32: LDS attribute");                         \
+        hipLaunchKernelGGL((ball_query_kernel<CP, CC, NW, PP, OT>), dim3((unsigned)nblk), dim3(64 * PP), \
+                           obytes, st, pp, cp_, (int)N, (int)S, (int)C, r2, (int)K, sm, out, cnt);     \
+    } while (0)
     if (P == 8) {
         if (nw == 1) PN2_BQ_L(1, 8);
         else if (nw == 2) PN2_BQ_L(2, 8);
@@ -242,9 +272,9 @@ extern "C" int pn2_ball_query_f32(const float *pts_packed, const float *ctr_pack
                                   stream);
 }
 
-extern "C" int pn2_ball_query_cnt_f32(const float *pts_packed, const float *ctr_packed, int64_t B,
-                                      int64_t N, int64_t S, int64_t C, double radius, int64_t K,
-                                      int64_t *out_idx, int32_t *out_cnt, void *stream) {
+template <typename OT>
+static int ball_query_impl(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N, int64_t S,
+                           int64_t C, double radius, int64_t K, OT *out_idx, int32_t *out_cnt, void *stream) {
     PN2_REQUIRE(pts_packed && ctr_packed && out_idx, "pn2_ball_query_f32: null pointer");
     PN2_REQUIRE(B >= 0 && N >= 1 && S >= 0 && C >= 1 && C <= kMaxC && K >= 1,
                 "pn2_ball_query_f32: bad shape B=%lld N=%lld S=%lld C=%lld K=%lld", (long long)B,
@@ -259,11 +289,23 @@ extern "C" int pn2_ball_query_cnt_f32(const float *pts_packed, const float *ctr_
     const int64_t cp = pn2_packed_stride(C);
 #define PN2_BQ(CPV, CC) \
     if (cp == CPV && (CC == 0 || (C == CC && S * N * C >= 400))) \
-        return launch_bq<CPV, CC>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
+        return launch_bq<CPV, CC, OT>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
     PN2_BQ(4, 3) PN2_BQ(12, 10)
     PN2_BQ(4, 0) PN2_BQ(8, 0) PN2_BQ(12, 0) PN2_BQ(16, 0) PN2_BQ(20, 0)
 #undef PN2_BQ
     return set_error(PN2_EUNSUPPORTED, "pn2_ball_query_f32: C=%lld", (long long)C);
+}
+
+extern "C" int pn2_ball_query_cnt_f32(const float *pts_packed, const float *ctr_packed, int64_t B,
+                                      int64_t N, int64_t S, int64_t C, double radius, int64_t K,
+                                      int64_t *out_idx, int32_t *out_cnt, void *stream) {
+    return ball_query_impl<int64_t>(pts_packed, ctr_packed, B, N, S, C, radius, K, out_idx, out_cnt, stream);
+}
+
+extern "C" int pn2_ball_query_i32(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N,
+                                  int64_t S, int64_t C, double radius, int64_t K, int32_t *out_idx,
+                                  int32_t *out_cnt, void *stream) {
+    return ball_query_impl<int32_t>(pts_packed, ctr_packed, B, N, S, C, radius, K, out_idx, out_cnt, stream);
 }
 
 // ------------------------------------------------------------------ square_distance

@@ -137,6 +137,11 @@ __device__ __forceinline__ T layout_sum(const T (&a)[CM], int C, int rule) {
     return rowsum4<CM>(a, C);
 }
 
+// neighbour index i of a group-mode source (int64 lists, or the int32 ones of pn2_ball_query_i32)
+__device__ __forceinline__ int src_index(const pn2_sa_src &s, int64_t i) {
+    return s.idx32 ? s.idx32[i] : (int)s.idx[i];
+}
+
 __host__ __device__ __forceinline__ int layout_kind(int64_t sn, int64_t sc) {
     return (sc != 1 && sn == 1) ? 1 : 0;  // 1: point-contiguous ("strided") rows
 }

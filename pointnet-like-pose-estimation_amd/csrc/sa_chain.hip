@@ -293,12 +293,12 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         const int k = (urow_e >> 4) & 15, nv = (urow_e & 7) + 1;
         g = valid ? c_g0 + (unsigned)(urow_e >> 8) : c_g0;
         const int j = kUnitRows * k + ((r & 7) < nv ? (r & 7) : 0);
-        n = valid ? (int)s.idx[(int64_t)g * A.K + j] : 0;
+        n = valid ? src_index(s, (int64_t)g * A.K + j) : 0;
     } else {
         const unsigned R = (unsigned)slab * 32u + (unsigned)r;
         valid = R < (unsigned)A.M;
         g = valid ? R / (unsigned)A.K : 0u;
-        n = valid ? (int)s.idx[R] : 0;
+        n = valid ? src_index(s, R) : 0;
     }
     // a centroid with no neighbour in its radius is padded with N (the ball query raises
     // PN2_DEVERR_NO_NEIGHBOUR): read point 0 there, never past the cloud

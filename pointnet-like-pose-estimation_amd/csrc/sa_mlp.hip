@@ -84,7 +84,7 @@ __device__ __forceinline__ void gather_rows(const MlpArgs &A, float *act, int *r
             if (s.mode == PN2_SRC_GROUP_XYZ_FIRST || s.mode == PN2_SRC_GROUP_FEAT_FIRST) {
                 const unsigned g = R / (unsigned)s.K;
                 b = (int)(g / (unsigned)s.S);
-                n = (int)s.idx[R];
+                n = src_index(s, R);
                 if ((unsigned)n >= (unsigned)s.N) n = 0;  // no-neighbour pad (PN2_DEVERR_NO_NEIGHBOUR)
             } else if (s.mode == PN2_SRC_GROUP_ALL) {
                 b = (int)(R / (unsigned)s.N);
@@ -763,7 +763,7 @@ static int validate(const pn2_sa_src *src, const pn2_mlp_layer *layers, int nlay
     switch (s.mode) {
     case PN2_SRC_GROUP_XYZ_FIRST:
     case PN2_SRC_GROUP_FEAT_FIRST:
-        PN2_REQUIRE(s.pts && s.ctr && s.idx && (s.D == 0 || s.feat), "pn2_sa_mlp_max_f32: group source");
+        PN2_REQUIRE(s.pts && s.ctr && (s.idx || s.idx32) && (s.D == 0 || s.feat), "pn2_sa_mlp_max_f32: group source");
         PN2_REQUIRE(s.B >= 0 && s.N >= 1 && s.S >= 1 && s.K >= 1 && s.C >= 1 && s.D >= 0,
                     "pn2_sa_mlp_max_f32: bad group shape");
         M = s.B * s.S * s.K; cin0 = s.C + s.D; K = s.K;

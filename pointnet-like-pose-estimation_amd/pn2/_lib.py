@@ -44,6 +44,7 @@ class SaSrc(ctypes.Structure):
         ("B", _i64), ("N", _i64), ("C", _i64), ("D", _i64), ("S", _i64), ("K", _i64),
         ("cnt", _vp),
         ("zero_out", _vp), ("zero_count", _i64),
+        ("idx32", _vp),
     ]
 
 
@@ -72,6 +73,7 @@ SIGNATURES = {
     "pn2_pack_points_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pn2_ball_query_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp]),
     "pn2_ball_query_cnt_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp, _vp]),
+    "pn2_ball_query_i32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp, _vp]),
     "pn2_square_distance_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pn2_index_points_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp]),
     "pn2_group_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
@@ -114,7 +116,7 @@ SIGNATURES = {
                                _int, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 _lib = None
 
 

@@ -182,22 +182,27 @@ def _(points):
 # ------------------------------------------------------------------------------ ball query
 def ball_query_direct(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, nsample: int,
                       with_count: bool = False):
-    """Packed points [B,N,cp] and centroids [B,S,cp] -> group_idx [B,S,nsample] int64, and with
-    with_count also the distinct neighbours per centroid, [B,S] int32 (entries past them repeat
-    entry 0; sa_mlp_max_direct(cnt=...) then computes only those rows)."""
+    """Packed points [B,N,cp] and centroids [B,S,cp] -> group_idx [B,S,nsample] int64 (the
+    reference's query_ball_point); with with_count the SA layers' fused-path form: the lists as
+    int32 (half the bytes; sa_mlp_max_direct reads either) and the distinct neighbours per
+    centroid, [B,S] int32 (entries past them repeat entry 0; sa_mlp_max_direct(cnt=...) then
+    computes only those rows)."""
     _dev(pts_packed, "pn2::ball_query")
     B, N, _ = pts_packed.shape
     S = ctr_packed.shape[1]
     if nsample > N:
         # the reference's `group_idx[mask] = group_first[mask]` fails the same way (:89)
         raise IndexError("query_ball_point: sample_number %d > number of points %d" % (nsample, N))
-    out = torch.empty(B, S, nsample, dtype=torch.int64, device=pts_packed.device)
+    out = torch.empty(B, S, nsample, dtype=torch.int32 if with_count else torch.int64,
+                      device=pts_packed.device)
     cnt = torch.empty(B, S, dtype=torch.int32, device=pts_packed.device) if with_count else None
     cp = pts_packed.shape[2]
-    _run("pn2_ball_query_f32", _L.pn2_ball_query_cnt_f32,
+    fn = _L.pn2_ball_query_i32 if with_count else _L.pn2_ball_query_cnt_f32
+    _run("pn2_ball_query_f32", fn,
          (pts_packed.data_ptr(), ctr_packed.data_ptr(), B, N, S, C, float(radius), nsample,
           out.data_ptr(), 0 if cnt is None else cnt.data_ptr(), _stream(pts_packed)),
-         pts_packed.device, nbytes=4.0 * cp * B * (N + S) + 8.0 * B * S * nsample,
+         pts_packed.device, nbytes=4.0 * cp * B * (N + S) + out.element_size() * B * S * nsample +
+         (4.0 * B * S if with_count else 0.0),
          flops=float(B) * S * N * (2 * C + 3))  # SURVEY §8(d): pairs x (2C + 3)
     return (out, cnt) if with_count else out
 
@@ -370,7 +375,10 @@ def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K, cnt=None):
     if centers is not None:
         s.ctr = centers.data_ptr()
     if idx is not None:
-        s.idx = idx.data_ptr()
+        if idx.dtype == torch.int32:
+            s.idx32 = idx.data_ptr()
+        else:
+            s.idx = idx.data_ptr()
     if rows is not None:
         s.rows = rows.data_ptr()
         s.rs = rows.stride(0)

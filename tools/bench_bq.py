@@ -39,32 +39,30 @@ def main():
         fidx, newp, cpk, ppk = ops.fps_direct(xd, S, start.to(dev))
         for radius, K in rks:
             want = oracle.query_ball_point(radius, K, x[:2], newp[:2].cpu())
-            ref, cnt = ops.ball_query_direct(ppk, cpk, C, radius, K, True)
-            for v in os.environ.get("BQ_MODES", "").split(","):  # PN2_BQ_MODE variants
-                if v:
-                    os.environ["PN2_BQ_MODE"] = v
-                else:
-                    os.environ.pop("PN2_BQ_MODE", None)
-                got = ops.ball_query_direct(ppk, cpk, C, radius, K)
-                # the count is the number of distinct entries before the padding starts
-                w = np.asarray(want)
-                wc = np.array([[min(K, int(np.argmax(np.r_[r[1:] == r[0], True])) + 1) if (r[1:] == r[0]).any() else K
-                                for r in bb] for bb in w])
-                ok = bool(np.array_equal(got[:2].cpu().numpy(), w)) and bool(torch.equal(got, ref))
+            ref, cnt = ops.ball_query_direct(ppk, cpk, C, radius, K, True)  # int32 lists
+            w = np.asarray(want)
+            # the count is the number of distinct entries before the padding starts
+            wc = np.array([[min(K, int(np.argmax(np.r_[r[1:] == r[0], True])) + 1) if (r[1:] == r[0]).any() else K
+                            for r in bb] for bb in w])
+            for v in ("int64", "int32"):
+                fused = v == "int32"
+                got = ops.ball_query_direct(ppk, cpk, C, radius, K, fused)
+                got = got[0] if fused else got
+                ok = bool(np.array_equal(got[:2].cpu().numpy(), w)) and bool(torch.equal(got.long(), ref.long()))
                 cnt_ok = bool(np.array_equal(cnt[:2].cpu().numpy(), wc))
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 reps = 20
                 e0.record()
                 for _ in range(reps):
-                    ops.ball_query_direct(ppk, cpk, C, radius, K)
+                    ops.ball_query_direct(ppk, cpk, C, radius, K, fused)
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / reps
                 pairs = float(B) * S * N
                 cp = ppk.shape[2]
-                nbytes = 4.0 * cp * B * (N + S) + 8.0 * B * S * K
-                r = {"shape": name, "radius": radius, "K": K, "mode": v or "default",
+                nbytes = 4.0 * cp * B * (N + S) + (4.0 if fused else 8.0) * B * S * K
+                r = {"shape": name, "radius": radius, "K": K, "out": v,
                      "us": round(us, 2), "exact": ok, "count_exact": cnt_ok,
                      "gpairs_per_s": round(pairs / us * 1e-3, 1),
                      "valu_frac": round(OPS_PER_PAIR * pairs / (us * 1e-6) / VALU_PEAK, 4),
