@@ -743,9 +743,13 @@ namespace pn2 {
 // (merged there by atomicMax).
 constexpr int kScanThreads = 1024;
 
+// Side job (pre-pass chains): the centroid term u of u_table_kernel for the cloud's groups, the
+// same fma chain (one launch fewer on the compute stream).
 __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
     const int *__restrict__ cnt, int S, int K, int wpc, int *__restrict__ units,
-    int2 *__restrict__ desc, float *__restrict__ out, int64_t ostride, int cout, int prow) {
+    int2 *__restrict__ desc, float *__restrict__ out, int64_t ostride, int cout, int prow,
+    const float *__restrict__ w0x, int w0x_row, int cout0, const float *__restrict__ ctr, int C,
+    float *__restrict__ u) {
     extern __shared__ int ssm[];
     int *st = ssm;            // [S] units of group s, then its first unit
     int *strad = st + S;      // [S] groups to zero
@@ -828,6 +832,18 @@ __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
     for (int e = tid; e < ns * cout; e += kScanThreads) {
         const int j = e / cout, c = e - j * cout;
         out[((int64_t)b * S + strad[j]) * ostride + c] = 0.f;
+    }
+    if (u) {
+        for (int e = tid; e < S * cout0; e += kScanThreads) {
+            const int64_t g = (int64_t)b * S + e / cout0;
+            const int c = e % cout0;
+            float acc = 0.f;
+            for (int k = 0; k < C; ++k) {
+                const int row = w0x_row + k;
+                acc = __builtin_fmaf(w0x[((int64_t)(row >> 1) * cout0 + c) * 2 + (row & 1)], ctr[g * C + k], acc);
+            }
+            u[g * cout0 + c] = acc;
+        }
     }
 }
 
@@ -985,10 +1001,12 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         const int rc = launch_layer0_prepass(s, layers[0], ws, st);
         if (rc != PN2_OK) return rc;
         const int64_t G = s.B * s.S, cout0 = layers[0].cout;
-        hipLaunchKernelGGL(u_table_kernel, dim3((unsigned)((G * cout0 + 255) / 256)), dim3(256), 0, st,
-                           layers[0].wt, (int)(layers[0].cin - s.C), (int)cout0, s.ctr, (int)s.C, G,
-                           utab);  // the fp32 image's rows are [features | xyz]
-        PN2_LAUNCH_CHECK("u_table_kernel");
+        if (!compact) {  // with compaction the scan kernel computes u as a side job
+            hipLaunchKernelGGL(u_table_kernel, dim3((unsigned)((G * cout0 + 255) / 256)), dim3(256), 0, st,
+                               layers[0].wt, (int)(layers[0].cin - s.C), (int)cout0, s.ctr, (int)s.C, G,
+                               utab);  // the fp32 image's rows are [features | xyz]
+            PN2_LAUNCH_CHECK("u_table_kernel");
+        }
         KB0M = -1;
     }
     const int wpc = compact ? (int)compact_wpc(s) : 0;
@@ -1028,7 +1046,8 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         (void)attr;
         hipLaunchKernelGGL(compact_scan_kernel, dim3((unsigned)s.B), dim3(kScanThreads), slds, st,
                            s.cnt, (int)s.S, (int)s.K, wpc, cunits, cdesc, out, ostride,
-                           (int)layers[2].cout, cprow);
+                           (int)layers[2].cout, cprow, layers[0].wt, (int)(layers[0].cin - s.C),
+                           (int)layers[0].cout, s.ctr, (int)s.C, utab);
         PN2_LAUNCH_CHECK("compact_scan_kernel");
     }
     ChainArgs A;
