@@ -45,6 +45,7 @@ stream when ``run`` is called.
 """
 import atexit
 import ctypes
+import os
 import time
 
 import torch
@@ -102,6 +103,14 @@ _XCDS = 8
 _extra = {}  # device -> (second geometry stream, second compute stream)
 
 
+def _hw_queues():
+    """Hardware queues per process the HIP runtime was started with (GPU_MAX_HW_QUEUES)."""
+    try:
+        return max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
+    except ValueError:
+        return 4
+
+
 def _streams(device, geometry_cus):
     key = (device, geometry_cus)
     if key not in _partitions and int(geometry_cus) <= 0:
@@ -125,12 +134,13 @@ def _streams(device, geometry_cus):
         # tuning tail_prio = 1: the tail (heads) at high priority as well (A/B)
         tail = torch.cuda.Stream(dev, priority=min(lo, hi) if tuning.get("tail_prio") else 0)
         main2 = torch.cuda.default_stream(dev)
+        tail2 = torch.cuda.Stream(dev, priority=min(lo, hi) if tuning.get("tail_prio") else 0)
         for st in (geo, main, tail):
             with torch.cuda.stream(st):
                 torch.zeros(1, device=dev)
             st.synchronize()
         _partitions[key] = (geo, main, tail, ())
-        _extra[device] = (geo2, main2)
+        _extra[device] = (geo2, main2, tail2)
     if key not in _partitions:
         ncu = _cu_count(device)
         per = max(1, min(int(geometry_cus) // _XCDS, ncu // _XCDS - 1))  # CUs per XCD
@@ -444,8 +454,11 @@ class GraphedPipeline(PipelinedForward):
         if compute_streams == 2 and geometry_cus > 0:
             raise ValueError("pn2.pipeline: compute_streams=2 needs shared CUs (geometry_cus=0)")
         self.compute_streams = int(compute_streams)
-        # the head graphs get the tail stream while the queues allow it
-        self.head_on_tail = (geometry_streams + self.compute_streams + 1 <= 4 and
+        # the head graphs get the tail stream(s) while the process's hardware queues allow it
+        # (GPU_MAX_HW_QUEUES, HIP's default 4; bench.py runs with 8): every stream on a queue
+        # of its own
+        self.tail_streams = 2 if int(tuning.get("tail_streams")) == 2 and geometry_cus <= 0 else 1
+        self.head_on_tail = (geometry_streams + self.compute_streams + self.tail_streams <= _hw_queues() and
                              not tuning.get("heads_on_compute"))  # A/B
         self.nslots = int(nslots)
         self.gb = gb
@@ -630,8 +643,9 @@ class GraphedPipeline(PipelinedForward):
         geo, main, tail = _streams(dev.index, self.geometry_cus)
         geos = [geo] + _extra_geometry_streams(dev.index, self.geometry_streams - 1)
         mains = [main] + ([_extra_compute_stream(dev.index)] if self.compute_streams == 2 else [])
+        tails = [tail] + ([_extra[dev.index][2]] if self.tail_streams == 2 else [])
         caller = torch.cuda.current_stream(dev)
-        for st in geos + mains + [tail]:
+        for st in geos + mains + tails:
             st.wait_stream(caller)
         # per group slot: the fps replay's event, and the events after which the group's
         # batches no longer read its inputs / geometry (one per batch: with two compute
@@ -710,8 +724,9 @@ class GraphedPipeline(PipelinedForward):
                 # the last `drain` batches run their heads on their own (by then idle)
                 # compute streams: the tail stream runs ~2 heads behind the sa graphs, and at
                 # the end of a run that backlog is the drain
-                ts = tail if (sl.head is not None and self.head_on_tail and
-                              i < len(batches) - drain) else main
+                # consecutive batches' heads alternate between the tail streams
+                ts = tails[(i - first) % len(tails)] if (sl.head is not None and self.head_on_tail and
+                                                         i < len(batches) - drain) else main
                 with torch.cuda.stream(ts):
                     if sl.head is not None:
                         if ts is not main:
@@ -723,11 +738,11 @@ class GraphedPipeline(PipelinedForward):
                     # replay does not wait for the collective; a later batch of the group
                     # replaces it (same streams, later in their order)
                     ev_read[s].append(ts.record_event() if sl.tail_reads_geometry else ev_sa)
-                    if post is not None and ts is tail:
+                    if post is not None and ts in tails:
                         out = post(i, out)
                     ev_head[bs] = ts.record_event()
                     mark(i - first, "hd1", ts)
-                if post is not None and ts is not tail:
+                if post is not None and ts not in tails:
                     # heads on the compute streams: `post` (e.g. the logits' all_gather) still
                     # runs on one stream in batch order, so every rank's collectives execute in
                     # the order they were issued
@@ -742,7 +757,7 @@ class GraphedPipeline(PipelinedForward):
         for g in geos[1:]:
             geo.wait_stream(g)
         self._pinned_evs[self._pinned_cur] = geo.record_event()  # uploads read it
-        for st in [geo] + mains + [tail]:
+        for st in [geo] + mains + tails:
             caller.wait_stream(st)
         return outs
 

@@ -18,6 +18,8 @@ Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_s
     geometry_stream  1: the eager forward runs layer i+1's FPS + ball query on a side stream
     fc_tail          0: the heads' FC tail as one row-kernel launch per layer + torch's
                      log_softmax / argmax, instead of pn2_fc_tail_f32's fused fc3 + log_softmax
+    tail_streams     2: the pipeline's heads alternate between two tail streams (needs the
+                     hardware queues: GPU_MAX_HW_QUEUES >= the pipeline's streams)
     force_gather     1: shard.all_gather_rows runs its collective in a 1-rank group too (the
                      bench's --force-rccl measurement of the collective's cost on one GPU)
 
@@ -36,6 +38,7 @@ HOST_DEFAULTS = {
     "geometry_stream": 0,
     "fc_tail": 1,
     "force_gather": 0,
+    "tail_streams": 1,
 }
 
 

@@ -429,7 +429,9 @@ def test_graphed_pipeline_delayed_tail_matches_eager(compute_streams, geometry_s
     gp = GraphedPipeline(model, tail=True, compute_streams=compute_streams,
                          geometry_streams=geometry_streams)
     assert gp._split_index() == 1  # sa3 (group_all) is in the head graph
-    assert gp.head_on_tail == (compute_streams + geometry_streams < 4)
+    from pn2 import pipeline
+    # the heads get their own stream(s) while every stream has a hardware queue
+    assert gp.head_on_tail == (compute_streams + geometry_streams + gp.tail_streams <= pipeline._hw_queues())
     torch.manual_seed(17)
     got = [o[1].cpu().numpy() for o in gp.run(xs, post=slow)]
     for i, (g, w) in enumerate(zip(got, want)):
