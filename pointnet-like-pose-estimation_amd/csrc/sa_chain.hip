@@ -741,7 +741,13 @@ namespace pn2 {
 // exclusive scan), 16 units per chain workgroup; the workgroup descriptors and unit table the
 // chain kernel reads; and a zeroed output row for every group whose units span two workgroups
 // (merged there by atomicMax).
-constexpr int kScanThreads = 1024;
+// 512 threads: in the pipeline the scan's workgroups wait for CU room beside the chains; 8-wave
+// workgroups get it sooner than 16-wave ones (SSG, interleaved A/B x3: 130.3-132.5k vs
+// 128.6-129.8k clouds/s with 1024, 128.7-130.9k with 256)
+#ifndef PN2_SCAN_THREADS
+#define PN2_SCAN_THREADS 512
+#endif
+constexpr int kScanThreads = PN2_SCAN_THREADS;
 
 // Side job (pre-pass chains): the centroid term u of u_table_kernel for the cloud's groups, the
 // same fma chain (one launch fewer on the compute stream).
