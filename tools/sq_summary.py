@@ -23,14 +23,18 @@ for k, v in agg.items():
     gui = c.get("GRBM_GUI_ACTIVE", 0)
     rows.append((gui, k, c, waves, wc))
 rows.sort(reverse=True)
-print("%-58s %6s %7s %6s %6s %6s %6s %7s %7s %7s %6s %6s" % (
-    "kernel", "waves", "gui_us", "wait", "winst", "active", "mfma", "valu/w", "salu/w", "lds/w", "vmrd/w", "ldsbc"))
+print("%-58s %6s %7s %6s %6s %6s %6s %7s %7s %7s %6s %6s %7s" % (
+    "kernel", "waves", "gui_us", "wait", "winst", "active", "mfma", "valu/w", "salu/w", "lds/w", "vmrd/w", "ldsbc",
+    "ldsact"))
 for gui, k, c, waves, wc in rows[:25]:
     mf = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
-    print("%-58s %6d %7.1f %6.2f %6.2f %6.2f %6s %7.0f %7.0f %7.0f %6.0f %6.3f" % (
+    lact = c.get("SQ_LDS_IDX_ACTIVE")
+    print("%-58s %6d %7.1f %6.2f %6.2f %6.2f %6s %7.0f %7.0f %7.0f %6.0f %6.3f %7s" % (
         k[:58], waves, gui / 8 / 2.4e3, c.get("SQ_WAIT_ANY", 0) / wc, c.get("SQ_WAIT_INST_ANY", 0) / wc,
         c.get("SQ_ACTIVE_INST_ANY", 0) / wc,
         "%.3f" % (mf / (gui / 8 * 1024)) if mf and gui else "-",
         c.get("SQ_INSTS_VALU", 0) / waves, c.get("SQ_INSTS_SALU", 0) / waves,
         c.get("SQ_INSTS_LDS", 0) / waves, c.get("SQ_INSTS_VMEM_RD", 0) / waves,
-        c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1, c.get("SQ_LDS_IDX_ACTIVE", 0))))
+        c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1, c.get("SQ_LDS_IDX_ACTIVE", 0)),
+        # LDS-array cycles per CU-cycle of the kernel (256 CUs): the LDS's busy fraction
+        "%.3f" % (lact / (gui / 8 * 256)) if lact and gui else "-"))
