@@ -46,6 +46,67 @@ def test_validation_errors_without_gpu():
     assert rc == -2 and b"unsupported C" in L.pn2_last_error()
 
 
+def test_workspace_queries_r03():
+    """Host-side size queries of this round's entry points (no device call)."""
+    from pn2 import _lib
+    L = _lib.load()
+    # FPS: register-resident shapes and the streamed kernel with LDS distances need none; past
+    # N = 40952 one word per point
+    assert L.pn2_fps_workspace_bytes(4, 16384, 3, 512) == 0
+    assert L.pn2_fps_workspace_bytes(4, 32768, 3, 512) == 0
+    assert L.pn2_fps_workspace_bytes(4, 50000, 3, 256) == 4 * 50000 * 4
+    assert L.pn2_fps_workspace_bytes(0, 0, 3, 1) == -1
+    # the FC tail: y1 and y2, each padded to 4 floats
+    assert L.pn2_fc_tail_workspace_bytes(32, 512, 256) == (32 * 512 + 32 * 256) * 4
+    assert L.pn2_fc_tail_workspace_bytes(5, 513, 255) == (((5 * 513 + 3) // 4 * 4) + ((5 * 255 + 3) // 4 * 4)) * 4
+    assert L.pn2_fc_tail_workspace_bytes(0, 1, 1) == -1
+
+
+def test_validation_errors_r03_without_gpu():
+    from pn2 import _lib
+    L = _lib.load()
+    # int32 ball query: the same shape checks as the int64 one
+    rc = L.pn2_ball_query_i32(1, 1, 2, 8, 4, 3, 0.2, 9, 1, None, None)
+    assert rc == -1 and b"sample_number 9 > N 8" in L.pn2_last_error()
+    # streamed FPS past N = 40952 without the workspace it needs
+    rc = L.pn2_fps_ws_f32(1, 2, 50000, 3, 150000, 3, 1, 1, 16, 1, None, None, None, None, 0, None)
+    assert rc == -1 and b"workspace" in L.pn2_last_error()
+    rc = L.pn2_fps_f32(1, 2, 50000, 3, 150000, 3, 1, 1, 16, 1, None, None, None, None)
+    assert rc == -1 and b"workspace" in L.pn2_last_error()
+    # FC tail: a row block's logits must fit its LDS
+    rc = L.pn2_fc_tail_f32(1, 1024, 2, 1024, 1, None, 512, 1, None, 256, 1, None, 5000, 1, 1, 5000, None,
+                           1 << 20, 1 << 30, None)
+    assert rc == -1 and b"N3" in L.pn2_last_error()
+
+
+def test_tuning_switch_keys():
+    """The one tuning switch: the C keys are readable / settable and unknown keys fail."""
+    import ctypes
+    from pn2 import _lib, tuning
+    L = _lib.load()
+    keys = L.pn2_tuning_keys().decode().split()
+    for k in ("mlp_f32", "compact", "bq_waves", "fps_threads", "fps_ppt", "dense_lds"):
+        assert k in keys
+    v = ctypes.c_int64(-1)
+    assert L.pn2_tuning_get(b"dense_lds", ctypes.byref(v)) == 0 and v.value == 0
+    assert L.pn2_tuning_set(b"no_such_key", 1) != 0
+    with tuning.override(fps_threads=512, tail_streams=2):
+        assert tuning.kernel("fps_threads") == 512 and tuning.get("tail_streams") == 2
+    assert tuning.kernel("fps_threads") == 0 and tuning.get("tail_streams") == 1
+
+
+def test_pipeline_queue_rule(monkeypatch):
+    """The pipeline gives the heads their tail stream(s) only while every stream has a hardware
+    queue (GPU_MAX_HW_QUEUES, HIP's default 4)."""
+    from pn2 import pipeline
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
+    assert pipeline._hw_queues() == 4
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
+    assert pipeline._hw_queues() == 8
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "junk")
+    assert pipeline._hw_queues() == 4
+
+
 def _layers(widths, cin):
     from pn2 import _lib
     arr = (_lib.MlpLayer * len(widths))()
