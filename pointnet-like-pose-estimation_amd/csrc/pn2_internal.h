@@ -34,8 +34,8 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(mlp_f32, 0)          /* 1: fp32 MFMA kernels instead of the split-bf16 ones          */ \
     X(chain_prepass, 1)    /* 0: no layer-0 pre-pass (wide first layers of a chain)        */ \
     X(compact, 1)          /* 0: no compact neighbourhoods (every padded row computed)     */ \
-    X(compact_pool, 0)     /* LDS pool rows of compact chain launches (0: automatic)       */ \
-    X(compact_stages, 2)   /* weight-ring stages of compact chain launches (2 or 3)        */ \
+    X(compact_pool, 16)     /* LDS pool rows of compact chain launches (0: automatic)       */ \
+    X(compact_stages, 3)   /* weight-ring stages of compact chain launches (2 or 3)        */ \
     X(bq_waves, 0)         /* ball query waves per workgroup (0: automatic, 8 or 16)       */ \
     X(fps_threads, 0)      /* FPS block shape threads x points per thread (0: automatic)   */ \
     X(fps_ppt, 0)                                                                              \

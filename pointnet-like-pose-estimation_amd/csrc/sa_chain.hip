@@ -1020,9 +1020,12 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     // 16-row pool a 3-stage ring cost a workgroup per CU (SSG sa2: 3 -> 2 live per CU, 114 ->
     // 130 us, although each workgroup lived 36 us instead of 45: tools/debug/chain_stamps.py).
     // An 8-row pool (groups past it merge through HBM atomics into rows the scan zeroed) keeps
-    // 3 per CU with 3 stages -- measured 117.8 vs 114.2 us, so the default stays 2 stages;
-    // tuning compact_stages = 3 selects the 3-stage ring with the 8-row pool when it keeps the
-    // workgroups per CU the registers allow (A/B, and the tests of the overflow path).
+    // 3 per CU with 3 stages: eager (each kernel alone) 117.8 vs 114.2 us, but in the pipeline,
+    // where the chains share CUs with the heads and the scans, the deeper ring wins.  Defaults
+    // (r03, interleaved A/B x4, SSG K = 100): tuning compact_pool = 16 (the full pool, one
+    // workgroup per CU fewer at sa1: 5 -> 4) and compact_stages = 3 (the 3-stage ring with the
+    // 8-row pool wherever it keeps the workgroups per CU, i.e. sa2): 132.2-133.2k vs
+    // 119.5-129.7k clouds/s; MSG / POSE / STRESS within noise.
     int cks = 2, cprow = kUnitsPerWG;
     if (compact) {
         const int64_t cL = layers[2].cout;
@@ -1032,10 +1035,12 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         auto wgs = [&](int ks, int prow) {
             return std::min<int64_t>(occ_v, (int64_t)(160 * 1024) / (int64_t)(prow * cL * 4 + bnb + ks * sb));
         };
-        // an 8-row pool when it buys a workgroup per CU (SSG sa1: 4 -> 5 per CU, 62.4 -> 59.9
-        // us; its many small groups past the 8th of a workgroup merge through HBM atomics)
+        // an 8-row pool when it buys a workgroup per CU (SSG sa1 eager: 4 -> 5 per CU, 62.4 ->
+        // 59.9 us; its many small groups past the 8th of a workgroup merge through HBM atomics)
+        // -- unless tuning compact_pool sets the pool rows (default 16: in the pipeline the
+        // full pool measured faster, see above)
         if (wgs(2, 8) > wgs(2, kUnitsPerWG)) cprow = 8;
-        if (tuning().compact_pool > 0)  // A/B override of the pool rows
+        if (tuning().compact_pool > 0)
             cprow = (int)std::max<int64_t>(1, std::min<int64_t>(kUnitsPerWG, tuning().compact_pool));
         if (tuning().compact_stages == 3 && wgs(3, 8) >= wgs(2, kUnitsPerWG))
             cks = 3, cprow = 8;

@@ -139,9 +139,10 @@ COMPACT = [
 ]
 
 
+@pytest.mark.parametrize("pool", [16, 0])  # the full LDS pool (default), or automatic (8 rows where that buys a workgroup)
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("case", range(len(COMPACT)))
-def test_compact_neighbourhoods_bit_exact(case, prec):
+def test_compact_neighbourhoods_bit_exact(case, prec, pool):
     """Computing only each group's distinct rows (8-row units, the padding repeats of the first
     neighbour dropped) gives the bits of the full K rows per group: every row's MLP is
     computed the same way, and the max is the same without repeats.  Covers K % 8 != 0, groups
@@ -172,7 +173,7 @@ def test_compact_neighbourhoods_bit_exact(case, prec):
     for mode in ("0", "1") if (chainable or prec == "fp32") else ("1",):
         torch.manual_seed(77)
         with torch.no_grad(), pn2.mlp_precision(prec), \
-                tuning.override(compact=int(mode), compact_stages=stages):
+                tuning.override(compact=int(mode), compact_stages=stages, compact_pool=pool):
             outs[mode] = sa(x, f)[1].cpu().numpy()
     if chainable:  # else the full-row launch is not the chain kernel (no bf16 kernel at all)
         np.testing.assert_array_equal(outs["1"].view(np.uint32), outs["0"].view(np.uint32))
