@@ -507,7 +507,8 @@ def main():
                    "kernel": "pn2_ball_query_f32 (ball_query_kernel)",
                    "flops_basis": "algorithmic: every centroid-point pair x (2C+3) (SURVEY 8(d)); the "
                                   "kernel stops a cloud's scan once all its centroids have K hits",
-                   "bytes_basis": "compulsory: packed points and centroids in, int64 [B,S,K] out",
+                   "bytes_basis": "compulsory: packed points and centroids in, the SA path's "
+                                  "int32 [B,S,K] lists and [B,S] counts out",
                    "avg_launch_ms": bq["ms"] / bq["launches"]}
 
     cpu = None

@@ -744,6 +744,9 @@ namespace pn2 {
 // 512 threads: in the pipeline the scan's workgroups wait for CU room beside the chains; 8-wave
 // workgroups get it sooner than 16-wave ones (SSG, interleaved A/B x3: 130.3-132.5k vs
 // 128.6-129.8k clouds/s with 1024, 128.7-130.9k with 256)
+#ifndef PN2_U_FOLD  // 0: the centroid term u as its own launch (u_table_kernel), for A/B builds
+#define PN2_U_FOLD 1
+#endif
 #ifndef PN2_SCAN_THREADS
 #define PN2_SCAN_THREADS 512
 #endif
@@ -764,6 +767,17 @@ __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b = blockIdx.x;
     const int *cb = cnt + (int64_t)b * S;
+    // side job's operands (W0's xyz rows, the cloud's centroids) staged in LDS behind the
+    // scan's own words, first, so their loads overlap the scan; read after its barriers
+    float *sw0 = reinterpret_cast<float *>(ssm + 2 * S + wpc + 32);  // [C][cout0]
+    float *sct = sw0 + C * cout0;                                     // [S][C]
+    if (u) {
+        for (int e = tid; e < C * cout0; e += kScanThreads) {
+            const int k = e / cout0, c = e - k * cout0, row = w0x_row + k;
+            sw0[e] = w0x[((int64_t)(row >> 1) * cout0 + c) * 2 + (row & 1)];
+        }
+        for (int e = tid; e < S * C; e += kScanThreads) sct[e] = ctr[(int64_t)b * S * C + e];
+    }
     const int per = (S + kScanThreads - 1) / kScanThreads;
     const int lo = min(S, tid * per), hi = min(S, lo + per);
     int sum = 0;
@@ -840,15 +854,14 @@ __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
         out[((int64_t)b * S + strad[j]) * ostride + c] = 0.f;
     }
     if (u) {
-        for (int e = tid; e < S * cout0; e += kScanThreads) {
-            const int64_t g = (int64_t)b * S + e / cout0;
-            const int c = e % cout0;
-            float acc = 0.f;
-            for (int k = 0; k < C; ++k) {
-                const int row = w0x_row + k;
-                acc = __builtin_fmaf(w0x[((int64_t)(row >> 1) * cout0 + c) * 2 + (row & 1)], ctr[g * C + k], acc);
+        // a group per wave, its outputs across the lanes (no per-element division)
+        for (int g = wave; g < S; g += kScanThreads / 64) {
+            float *ur = u + ((int64_t)b * S + g) * cout0;
+            for (int c = lane; c < cout0; c += 64) {
+                float acc = 0.f;
+                for (int k = 0; k < C; ++k) acc = __builtin_fmaf(sw0[k * cout0 + c], sct[g * C + k], acc);
+                ur[c] = acc;
             }
-            u[g * cout0 + c] = acc;
         }
     }
 }
@@ -1007,7 +1020,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         const int rc = launch_layer0_prepass(s, layers[0], ws, st);
         if (rc != PN2_OK) return rc;
         const int64_t G = s.B * s.S, cout0 = layers[0].cout;
-        if (!compact) {  // with compaction the scan kernel computes u as a side job
+        if (!compact || !PN2_U_FOLD) {  // with compaction the scan kernel computes u as a side job
             hipLaunchKernelGGL(u_table_kernel, dim3((unsigned)((G * cout0 + 255) / 256)), dim3(256), 0, st,
                                layers[0].wt, (int)(layers[0].cin - s.C), (int)cout0, s.ctr, (int)s.C, G,
                                utab);  // the fp32 image's rows are [features | xyz]
@@ -1050,7 +1063,8 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     if (compact) {
         cunits = reinterpret_cast<int *>(reinterpret_cast<char *>(ws) + zb);
         cdesc = reinterpret_cast<int2 *>(cunits + s.B * wpc * kUnitsPerWG);
-        const size_t slds = compact_scan_lds(s);
+        // + the centroid-term side job's staged W0 xyz rows and centroids
+        const size_t slds = compact_scan_lds(s) + (utab && PN2_U_FOLD ? (size_t)(s.C * layers[0].cout + s.S * s.C) * 4 : 0);
         static const hipError_t attr = hipFuncSetAttribute(
             reinterpret_cast<const void *>(&compact_scan_kernel),
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1058,7 +1072,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         hipLaunchKernelGGL(compact_scan_kernel, dim3((unsigned)s.B), dim3(kScanThreads), slds, st,
                            s.cnt, (int)s.S, (int)s.K, wpc, cunits, cdesc, out, ostride,
                            (int)layers[2].cout, cprow, layers[0].wt, (int)(layers[0].cin - s.C),
-                           (int)layers[0].cout, s.ctr, (int)s.C, utab);
+                           (int)layers[0].cout, s.ctr, (int)s.C, PN2_U_FOLD ? utab : nullptr);
         PN2_LAUNCH_CHECK("compact_scan_kernel");
     }
     ChainArgs A;
