@@ -38,8 +38,12 @@ gp.trace = []
 t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 if os.environ.get("FROM_START"):  # a timed run as the bench times it: K batches from idle
     t_start.record()
+    import time
+    h_start = time.perf_counter()
     gp.run([x] * K, None if ex is None else ex * K)
     t_end.record()
+    print("host: geo0 issued %.1f us, sa0 issued %.1f us after run() was called" % (
+        (gp.trace[0]["geo0"][1] - h_start) * 1e6, (gp.trace[0]["sa0"][1] - h_start) * 1e6))
     torch.cuda.synchronize()
     tr = gp.trace
     print("whole run %.1f us for %d batches (%.0f clouds/s)" % (
