@@ -63,7 +63,7 @@ struct ChainArgs {
     int lds_ring;  // byte offset of the workgroup weight ring (kStages stage buffers)
     // KB0M < 0 (layer 0 pre-transformed): z [B*N][32*T0] = W0 . [xyz | features] of every source
     // point (launch_layer0_prepass); u [B*S][32*T0] = W0_xyz . centroid of every group
-    // (u_table_kernel)
+    // (u_table_kernel, or compact_scan_kernel's extra workgroups)
     const float *z;
     const float *u;
     // compact neighbourhoods (pool_mode 3, given the ball query's distinct-neighbour counts): a
@@ -744,21 +744,59 @@ namespace pn2 {
 // 512 threads: in the pipeline the scan's workgroups wait for CU room beside the chains; 8-wave
 // workgroups get it sooner than 16-wave ones (SSG, interleaved A/B x3: 130.3-132.5k vs
 // 128.6-129.8k clouds/s with 1024, 128.7-130.9k with 256)
-#ifndef PN2_U_FOLD  // 0: the centroid term u as its own launch (u_table_kernel), for A/B builds
-#define PN2_U_FOLD 1
-#endif
 #ifndef PN2_SCAN_THREADS
 #define PN2_SCAN_THREADS 512
 #endif
 constexpr int kScanThreads = PN2_SCAN_THREADS;
 
-// Side job (pre-pass chains): the centroid term u of u_table_kernel for the cloud's groups, the
-// same fma chain (one launch fewer on the compute stream).
+// Pre-pass chains: workgroups B .. B + gridDim.x - 1 of the same launch compute the centroid
+// term u [g][c] = sum_k W0[c][xyz k] * centroid[g][k] (k ascending, one fma chain from 0), the
+// centroid's share of layer 0 that the per-point z cannot subtract (W0's fp32 image is
+// pair-interleaved [cin_pad/2][cout0][2], its xyz rows from w0x_row).  One launch fewer on the
+// compute stream than a u kernel of its own (4.8 us); as a job of the B scan workgroups it made
+// the launch 6 -> 22 us (SSG sa2, eager), on the chain's critical path.
 __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
-    const int *__restrict__ cnt, int S, int K, int wpc, int *__restrict__ units,
+    const int *__restrict__ cnt, int B, int S, int K, int wpc, int *__restrict__ units,
     int2 *__restrict__ desc, float *__restrict__ out, int64_t ostride, int cout, int prow,
     const float *__restrict__ w0x, int w0x_row, int cout0, const float *__restrict__ ctr, int C,
     float *__restrict__ u) {
+    if ((int)blockIdx.x >= B) {
+        // a contiguous range of groups per workgroup; thread t keeps output column t % cout0
+        // (its W0 xyz weights in registers) over groups t / cout0, + kScanThreads / cout0, ...
+        const int G = B * S, nwg = gridDim.x - B;
+        const int gper = (G + nwg - 1) / nwg, g0 = ((int)blockIdx.x - B) * gper;
+        const int g1 = min(G, g0 + gper);
+        const int tid = threadIdx.x;
+        if (kScanThreads % cout0 == 0 && C <= kMaxC) {
+            const int c = tid % cout0, gstep = kScanThreads / cout0;
+            float w[kMaxC];
+#pragma unroll
+            for (int k = 0; k < kMaxC; ++k) {
+                const int row = w0x_row + k;
+                w[k] = k < C ? w0x[((int64_t)(row >> 1) * cout0 + c) * 2 + (row & 1)] : 0.f;
+            }
+            for (int g = g0 + tid / cout0; g < g1; g += gstep) {
+                const float *cg = ctr + (int64_t)g * C;
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < kMaxC; ++k)
+                    if (k < C) acc = __builtin_fmaf(w[k], cg[k], acc);
+                u[(int64_t)g * cout0 + c] = acc;
+            }
+        } else {
+            for (int e = tid; e < (g1 - g0) * cout0; e += kScanThreads) {
+                const int g = g0 + e / cout0, c = e % cout0;
+                float acc = 0.f;
+                for (int k = 0; k < C; ++k) {
+                    const int row = w0x_row + k;
+                    acc = __builtin_fmaf(w0x[((int64_t)(row >> 1) * cout0 + c) * 2 + (row & 1)],
+                                         ctr[(int64_t)g * C + k], acc);
+                }
+                u[(int64_t)g * cout0 + c] = acc;
+            }
+        }
+        return;
+    }
     extern __shared__ int ssm[];
     int *st = ssm;            // [S] units of group s, then its first unit
     int *strad = st + S;      // [S] groups to zero
@@ -767,17 +805,6 @@ __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b = blockIdx.x;
     const int *cb = cnt + (int64_t)b * S;
-    // side job's operands (W0's xyz rows, the cloud's centroids) staged in LDS behind the
-    // scan's own words, first, so their loads overlap the scan; read after its barriers
-    float *sw0 = reinterpret_cast<float *>(ssm + 2 * S + wpc + 32);  // [C][cout0]
-    float *sct = sw0 + C * cout0;                                     // [S][C]
-    if (u) {
-        for (int e = tid; e < C * cout0; e += kScanThreads) {
-            const int k = e / cout0, c = e - k * cout0, row = w0x_row + k;
-            sw0[e] = w0x[((int64_t)(row >> 1) * cout0 + c) * 2 + (row & 1)];
-        }
-        for (int e = tid; e < S * C; e += kScanThreads) sct[e] = ctr[(int64_t)b * S * C + e];
-    }
     const int per = (S + kScanThreads - 1) / kScanThreads;
     const int lo = min(S, tid * per), hi = min(S, lo + per);
     int sum = 0;
@@ -853,22 +880,9 @@ __global__ __launch_bounds__(kScanThreads) void compact_scan_kernel(
         const int j = e / cout, c = e - j * cout;
         out[((int64_t)b * S + strad[j]) * ostride + c] = 0.f;
     }
-    if (u) {
-        // a group per wave, its outputs across the lanes (no per-element division)
-        for (int g = wave; g < S; g += kScanThreads / 64) {
-            float *ur = u + ((int64_t)b * S + g) * cout0;
-            for (int c = lane; c < cout0; c += 64) {
-                float acc = 0.f;
-                for (int k = 0; k < C; ++k) acc = __builtin_fmaf(sw0[k * cout0 + c], sct[g * C + k], acc);
-                ur[c] = acc;
-            }
-        }
-    }
 }
 
-// u [g][c] = sum_k W0[c][xyz k] * centroid[g][k] (k ascending, one fma chain from 0): the
-// centroid's share of layer 0, which the per-point pre-pass z could not subtract.  W0's fp32
-// image is pair-interleaved [cin_pad/2][cout][2]; its xyz rows start at w0x_row.
+// u without compaction: the same fma chain as compact_scan_kernel's u workgroups
 __global__ __launch_bounds__(256) void u_table_kernel(const float *__restrict__ w0x, int w0x_row,
                                                       int cout, const float *__restrict__ ctr,
                                                       int C, int64_t G, float *__restrict__ u) {
@@ -1011,7 +1025,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     bool compact = pool && chain_use_compact(s) && ws && ((uintptr_t)ws & 15) == 0 &&
                    ws_bytes >= zb + compact_table_bytes(s);
     // With the layer-0 pre-pass (wide first layers: SSG / pose sa2) compaction paid only once
-    // the centroid term u came from a global table (u_table_kernel) instead of being computed
+    // the centroid term u came from a global table instead of being computed
     // per workgroup for its 16 groups (setup 8.8 us of a 49 us workgroup life,
     // tools/debug/chain_stamps.py): SSG sa2 115 us vs 130 us computing the padding rows.
     float *utab = pre ? reinterpret_cast<float *>(reinterpret_cast<char *>(ws) + prepass_z_bytes(s, layers[0]))
@@ -1019,8 +1033,8 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     if (pre) {
         const int rc = launch_layer0_prepass(s, layers[0], ws, st);
         if (rc != PN2_OK) return rc;
-        const int64_t G = s.B * s.S, cout0 = layers[0].cout;
-        if (!compact || !PN2_U_FOLD) {  // with compaction the scan kernel computes u as a side job
+        if (!compact) {  // with compaction the scan launch's extra workgroups compute u
+            const int64_t G = s.B * s.S, cout0 = layers[0].cout;
             hipLaunchKernelGGL(u_table_kernel, dim3((unsigned)((G * cout0 + 255) / 256)), dim3(256), 0, st,
                                layers[0].wt, (int)(layers[0].cin - s.C), (int)cout0, s.ctr, (int)s.C, G,
                                utab);  // the fp32 image's rows are [features | xyz]
@@ -1063,16 +1077,19 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     if (compact) {
         cunits = reinterpret_cast<int *>(reinterpret_cast<char *>(ws) + zb);
         cdesc = reinterpret_cast<int2 *>(cunits + s.B * wpc * kUnitsPerWG);
-        // + the centroid-term side job's staged W0 xyz rows and centroids
-        const size_t slds = compact_scan_lds(s) + (utab && PN2_U_FOLD ? (size_t)(s.C * layers[0].cout + s.S * s.C) * 4 : 0);
+        const size_t slds = compact_scan_lds(s);
+        // u's workgroups (pre-pass chains): ~4 outputs per thread
+        const int64_t ut = utab ? s.B * s.S * layers[0].cout : 0;
+        const unsigned nu = (unsigned)std::min<int64_t>(std::min<int64_t>(1024, s.B * s.S),
+                                                        (ut + 4 * kScanThreads - 1) / (4 * kScanThreads));
         static const hipError_t attr = hipFuncSetAttribute(
             reinterpret_cast<const void *>(&compact_scan_kernel),
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)attr;
-        hipLaunchKernelGGL(compact_scan_kernel, dim3((unsigned)s.B), dim3(kScanThreads), slds, st,
-                           s.cnt, (int)s.S, (int)s.K, wpc, cunits, cdesc, out, ostride,
+        hipLaunchKernelGGL(compact_scan_kernel, dim3((unsigned)s.B + nu), dim3(kScanThreads), slds, st,
+                           s.cnt, (int)s.B, (int)s.S, (int)s.K, wpc, cunits, cdesc, out, ostride,
                            (int)layers[2].cout, cprow, layers[0].wt, (int)(layers[0].cin - s.C),
-                           (int)layers[0].cout, s.ctr, (int)s.C, PN2_U_FOLD ? utab : nullptr);
+                           (int)layers[0].cout, s.ctr, (int)s.C, utab);
         PN2_LAUNCH_CHECK("compact_scan_kernel");
     }
     ChainArgs A;
