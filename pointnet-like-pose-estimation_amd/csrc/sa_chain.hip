@@ -1015,6 +1015,11 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     if (!chain_shape(s, layers, nlayers, pool, T0, T1, kbs)) return 0;
     int KB0M = chain_kb0m(T0, T1, kbs[0]);
     if (KB0M < 0) return 0;
+    // bf16 chains stream a multi-block layer-0 input rather than hold it resident: the
+    // resident block takes the VGPRs of a wave per SIMD (STRESS sa2 (4,4): 144 -> 112 VGPRs,
+    // 3 -> 4 waves/SIMD; eager 265 -> 193 us, pipelined STRESS 124.6k -> 130.1k clouds/s).  The
+    // split (fp32) chains gain nothing: (4,4,9) 158, (4,4,0) 151 VGPRs, both 3 waves/SIMD.
+    if (np == 1 && KB0M > 1 && chain_kb0m(T0, T1, 1 << 20) == 0) KB0M = 0;
     // without compaction a 32-row slab must hold rows of one group (K = 8, 16: several whole
     // groups; K % 32 == 0: part of one)
     if (!(pool && chain_use_compact(s)) && !(K == 8 || K == 16 || K % 32 == 0)) return 0;

@@ -826,30 +826,47 @@ static int launch_dense_lds_tile(int tile, const DenseSplitArgs &A, int np, hipS
     }
 }
 
-// Large layers take 256 x 128 tiles (see dense_split_layer); the rows a launch's workgroup
-// covers decide which pools fit in LDS
-static bool dense_wide(const DenseSplitArgs &A) {
+// Large split (fp32-accurate) layers take 256 x 128 tiles (see dense_split_layer); the rows a
+// launch's workgroup covers decide which pools fit in LDS.  bf16 layers keep the 128-row tiles:
+// with one MFMA per product instead of six the big tile's one workgroup per CU (8 waves, 221
+// VGPRs) is load-latency bound -- STRESS (sa3 512 -> 1024 over 16384 rows, pipelined) 129.3-132.5k
+// with it, 134.1-135.6k without (interleaved A/B x3).
+static bool dense_wide(const DenseSplitArgs &A, int np) {
     const int64_t wide_min = tuning().dense_wide_minwg;
-    return A.tiles % 4 == 0 && (A.M + 255) / 256 * (A.tiles / 4) >= wide_min;
+    return np == 3 && A.tiles % 4 == 0 && (A.M + 255) / 256 * (A.tiles / 4) >= wide_min;
 }
-static int dense_pool_mode(const DenseSplitArgs &A) {
-    const int64_t kRowsSel = dense_wide(A) ? 256 : kDRows;
+// the 4-wave tile's column tiles per wave: the widest that still leaves dense_minwg workgroups
+static int dense_ntc(const DenseSplitArgs &A) {
+    const int64_t rowblocks = (A.M + kDRows - 1) / kDRows;
+    const int64_t min_wg = tuning().dense_minwg;
+    for (int t = (int)tuning().dense_maxntc; t > 1; t /= 2)
+        if (A.tiles % t == 0 && rowblocks * (A.tiles / t) >= min_wg) return t;
+    return 1;
+}
+// tuning dense_w8 = n > 0: a 2-column-tile layer runs as 8-wave 256 x 64 tiles (one LDS weight
+// stage shared by 8 waves) when that still leaves n workgroups
+static bool dense_w8(const DenseSplitArgs &A, int np) {
+    const int64_t n = tuning().dense_w8;
+    return n > 0 && !dense_wide(A, np) && dense_ntc(A) == 2 && (A.M + 255) / 256 * (A.tiles / 2) >= n;
+}
+static int dense_pool_mode(const DenseSplitArgs &A, int np) {
+    const int64_t kRowsSel = dense_wide(A, np) || dense_w8(A, np) ? 256 : kDRows;
     if (A.K == 8 || A.K == 16) return 0;
     if (A.K % 32 == 0 && kRowsSel % A.K == 0) return 1;
     return 2;
 }
 
 // whether the layer, as it will be launched, pools through HBM atomics into a zeroed output
-static bool dense_needs_zero(const DenseSplitArgs &A) {
+static bool dense_needs_zero(const DenseSplitArgs &A, int np) {
     if (!A.pool) return false;
     const int tile = dense_lds_tile(A);
     if (tile) return (32 * (tile / 10)) % A.K != 0;
-    return dense_pool_mode(A) == 2;
+    return dense_pool_mode(A, np) == 2;
 }
 
 static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st, bool prezeroed = false) {
     if (const int tile = dense_lds_tile(A)) {
-        const bool hbm = dense_needs_zero(A);
+        const bool hbm = dense_needs_zero(A, np);
         const int64_t G = A.pool ? A.M / A.K : 0, cols = 32 * (int64_t)A.tiles;
         if (hbm && !prezeroed) {
             hipError_t e = A.ostride == cols
@@ -869,19 +886,11 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st, bool pre
     // waves of 32 rows x 4 column tiles): the 128 x 64 tile re-reads its A rows once per 64
     // output columns and its weights once per 128 rows, and at these sizes that L2 -> CU
     // stream, not the MFMA, was the bound.  Only when they still leave wide_min workgroups.
-    const bool wide = dense_wide(A);
+    const bool wide = dense_wide(A, np), w8 = dense_w8(A, np);
     // otherwise the widest tile (NTC 32-column tiles per wave) that still leaves min_wg workgroups
-    const int64_t rowblocks = (A.M + kDRows - 1) / kDRows;
-    const int64_t min_wg = tuning().dense_minwg;
-    const int max_ntc = (int)tuning().dense_maxntc;
-    int ntc = 1;
-    for (int t = max_ntc; t > 1; t /= 2)
-        if (A.tiles % t == 0 && rowblocks * (A.tiles / t) >= min_wg) {
-            ntc = t;
-            break;
-        }
+    const int ntc = dense_ntc(A);
     if (A.pool) {
-        A.pool_mode = dense_pool_mode(A);
+        A.pool_mode = dense_pool_mode(A, np);
         if (A.pool_mode == 2 && !prezeroed) {
             const int64_t G = A.M / A.K, cols = 32 * (int64_t)A.tiles;
             hipError_t e = A.ostride == cols
@@ -892,6 +901,7 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st, bool pre
     }
     int rc;
     if (wide) rc = np == 1 ? launch_dense_split<4, 1, 8>(A, st) : launch_dense_split<4, 3, 8>(A, st);
+    else if (w8) rc = np == 1 ? launch_dense_split<2, 1, 8>(A, st) : launch_dense_split<2, 3, 8>(A, st);
     else if (np == 1) rc = ntc == 4 ? launch_dense_split<4, 1>(A, st) : ntc == 2 ? launch_dense_split<2, 1>(A, st)
                                                                       : launch_dense_split<1, 1>(A, st);
     else rc = ntc == 4 ? launch_dense_split<4, 3>(A, st) : ntc == 2 ? launch_dense_split<2, 3>(A, st)
@@ -988,7 +998,7 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
     // a last layer that pools by HBM atomics gets its output zeroed by the layer before it
     // (one launch fewer than a memset: PointNet-v1's max over N points, group_all over K > 256)
     DenseSplitArgs last = make(nlayers - 1);
-    const bool fold_zero = nlayers > 1 && last.pool && dense_needs_zero(last);
+    const bool fold_zero = nlayers > 1 && last.pool && dense_needs_zero(last, np);
     if (s.zero_out && s.zero_count > 0) {  // the caller's side job rides on the last layer
         last.zero = s.zero_out;
         last.zrows = 1;
