@@ -42,7 +42,6 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(dense_maxntc, 2)     /* widest 32-column tile count of the 4-wave dense layer         */ \
     X(dense_minwg, 256)    /* workgroups a wider dense tile must still leave                 */ \
     X(dense_wide_minwg, 512) /* workgroups the 256 x 128 dense tile must leave              */ \
-    X(dense_w8, 0)         /* n > 0: 8-wave 256 x 64 dense tiles where >= n workgroups remain */ \
     X(dense_lds, 0)        /* 1: LDS-staged dense kernel (faster alone, slower pipelined)   */ \
     X(dense_lds_stages, 3) /* ring stages of the LDS-staged dense kernel (3 or 4)            */ \
     X(dense_lds_xcd2d, 0)  /* 1: XCD rectangles of row blocks x column tiles                */ \

@@ -843,14 +843,8 @@ static int dense_ntc(const DenseSplitArgs &A) {
         if (A.tiles % t == 0 && rowblocks * (A.tiles / t) >= min_wg) return t;
     return 1;
 }
-// tuning dense_w8 = n > 0: a 2-column-tile layer runs as 8-wave 256 x 64 tiles (one LDS weight
-// stage shared by 8 waves) when that still leaves n workgroups
-static bool dense_w8(const DenseSplitArgs &A, int np) {
-    const int64_t n = tuning().dense_w8;
-    return n > 0 && !dense_wide(A, np) && dense_ntc(A) == 2 && (A.M + 255) / 256 * (A.tiles / 2) >= n;
-}
 static int dense_pool_mode(const DenseSplitArgs &A, int np) {
-    const int64_t kRowsSel = dense_wide(A, np) || dense_w8(A, np) ? 256 : kDRows;
+    const int64_t kRowsSel = dense_wide(A, np) ? 256 : kDRows;
     if (A.K == 8 || A.K == 16) return 0;
     if (A.K % 32 == 0 && kRowsSel % A.K == 0) return 1;
     return 2;
@@ -886,7 +880,7 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st, bool pre
     // waves of 32 rows x 4 column tiles): the 128 x 64 tile re-reads its A rows once per 64
     // output columns and its weights once per 128 rows, and at these sizes that L2 -> CU
     // stream, not the MFMA, was the bound.  Only when they still leave wide_min workgroups.
-    const bool wide = dense_wide(A, np), w8 = dense_w8(A, np);
+    const bool wide = dense_wide(A, np);
     // otherwise the widest tile (NTC 32-column tiles per wave) that still leaves min_wg workgroups
     const int ntc = dense_ntc(A);
     if (A.pool) {
@@ -901,7 +895,6 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st, bool pre
     }
     int rc;
     if (wide) rc = np == 1 ? launch_dense_split<4, 1, 8>(A, st) : launch_dense_split<4, 3, 8>(A, st);
-    else if (w8) rc = np == 1 ? launch_dense_split<2, 1, 8>(A, st) : launch_dense_split<2, 3, 8>(A, st);
     else if (np == 1) rc = ntc == 4 ? launch_dense_split<4, 1>(A, st) : ntc == 2 ? launch_dense_split<2, 1>(A, st)
                                                                       : launch_dense_split<1, 1>(A, st);
     else rc = ntc == 4 ? launch_dense_split<4, 3>(A, st) : ntc == 2 ? launch_dense_split<2, 3>(A, st)
