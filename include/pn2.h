@@ -120,7 +120,9 @@ int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64
 /* query_ball_point: for every centroid, the first K point indices (ascending) whose
  * square_distance is not > (float)(radius*radius), padded with the first hit (N if none).
  * pts_packed [B,N,cp], ctr_packed [B,S,cp] from pn2_pack_points_f32 / pn2_fps_f32.
- * out_idx [B,S,K] int64.  K > N is rejected with PN2_EINVAL (the reference raises IndexError). */
+ * out_idx [B,S,K] int64.  Any 1 <= K <= N (rows that fit a 96 KB LDS buffer are built there and
+ * written out whole; longer ones are written in place).  K > N is rejected with PN2_EINVAL
+ * (the reference raises IndexError). */
 int pn2_ball_query_f32(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N,
                        int64_t S, int64_t C, double radius, int64_t K, int64_t *out_idx,
                        void *stream);

@@ -85,10 +85,13 @@ __device__ __forceinline__ void bq_insert(unsigned &wd, float d, float r2) {
 }
 
 // OT: the index type written (int64: the reference's query_ball_point; int32: the SA path's
-// lists, half the bytes).  Each lane's hits go to its centroid's row of an LDS buffer
+// lists, half the bytes).  ROWBUF: each lane's hits go to its centroid's row of an LDS buffer
 // (64 rows of K + 1 entries, dynamic LDS); after the scan every row is written out whole,
-// padding included, one coalesced row per wave step.
-template <int CP, int CC, int NW, int P, typename OT>
+// padding included, one coalesced row per wave step.  !ROWBUF (rows too long for LDS, any
+// K <= N as the reference's slice [:, :, :nsample] allows, pointnet2_utils.py:87): a hit goes
+// straight to its slot of the output row (the slot is known from the prefix), the row's first
+// hit is kept in LDS for the padding, and only the padding is written in the coalesced pass.
+template <int CP, int CC, int NW, int P, typename OT, bool ROWBUF>
 __global__ __launch_bounds__(64 * P) void ball_query_kernel(
     const float *__restrict__ pts, const float *__restrict__ ctr, int N, int S, int C_, float r2,
     int K, int small_, OT *__restrict__ out, int *__restrict__ out_cnt) {
@@ -98,6 +101,7 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
     const int C = CC > 0 ? CC : C_;
     const bool small = CC > 0 ? false : small_;  // the specialised instances never see tiny shapes
     __shared__ int cnts[2][P][64];
+    __shared__ int first[64];  // !ROWBUF: each row's first hit (slot 0)
     extern __shared__ __attribute__((aligned(16))) char bq_dyn[];
     OT *obuf = reinterpret_cast<OT *>(bq_dyn);  // [64][K + 1]
     const int KP = K + 1;
@@ -193,13 +197,19 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
             round += x;
         }
         // this segment's hits, in index order, into the slots [off, K)
+        OT *orow = out + q * K;  // !ROWBUF (invalid lanes start at total = K: no writes)
 #pragma unroll
         for (int t = 0; t < NW; ++t) {
             unsigned wd = bits[t];
             while (wd != 0 && off < K) {
                 const int i = __builtin_clz(wd);
                 const int n = seg0 + 32 * t + i;
-                obuf[lane * KP + off] = (OT)n;
+                if constexpr (ROWBUF) {
+                    obuf[lane * KP + off] = (OT)n;
+                } else {
+                    orow[off] = (OT)n;
+                    if (off == 0) first[lane] = n;
+                }
                 ++off;
                 wd ^= 0x80000000u >> i;
             }
@@ -214,10 +224,14 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
     for (int j = w; j < 64; j += P) {
         if (g0 + j >= S) break;
         const int cj = min(__builtin_amdgcn_readlane(total, j), K);
-        const OT fj = cj > 0 ? obuf[j * KP] : (OT)N;
+        const OT fj = cj > 0 ? (ROWBUF ? obuf[j * KP] : (OT)first[j]) : (OT)N;
         if (cj == 0 && lane == 0) atomicOr(&g_bq_errors, (unsigned)PN2_DEVERR_NO_NEIGHBOUR);
         OT *o = out + ((int64_t)b * S + g0 + j) * K;
-        for (int k = lane; k < K; k += 64) o[k] = k < cj ? obuf[j * KP + k] : fj;
+        if constexpr (ROWBUF) {
+            for (int k = lane; k < K; k += 64) o[k] = k < cj ? obuf[j * KP + k] : fj;
+        } else {
+            for (int k = cj + lane; k < K; k += 64) o[k] = fj;  // the hits are already out
+        }
         if (out_cnt && lane == 0) out_cnt[(int64_t)b * S + g0 + j] = cj;
     }
 }
@@ -240,16 +254,25 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
     int nw = per_wave <= 32 ? 1 : per_wave <= 64 ? 2 : 4;
     if (CP > 4 && nw > 2) nw = 2;
     const int sm = (int)(S * N * C < 400);
+    // rows in an LDS buffer while it stays within bq_rowbuf_kb (<= 96 KB: with the tile and
+    // the counts that still fits a CU), else hits straight to HBM
     const size_t obytes = (size_t)64 * (K + 1) * sizeof(OT);
-    PN2_REQUIRE(obytes <= 96 * 1024, "pn2_ball_query_f32: K=%lld too large", (long long)K);
-#define PN2_BQ_L(NW, PP)                                                                               \
+    const int64_t rb_kb = tuning().bq_rowbuf_kb < 96 ? tuning().bq_rowbuf_kb : 96;
+    const bool rowbuf = obytes <= (size_t)rb_kb * 1024;
+#define PN2_BQ_L2(NW, PP, RB)                                                                          \
     do {                                                                                               \
         static const hipError_t attr = hipFuncSetAttribute(                                           \
-            reinterpret_cast<const void *>(&ball_query_kernel<CP, CC, NW, PP, OT>),                   \
+            reinterpret_cast<const void *>(&ball_query_kernel<CP, CC, NW, PP, OT, RB>),               \
             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);                                   \
         PN2_REQUIRE(attr == hipSuccess, "pn2_ball_query_f32: LDS attribute");                         \
-        hipLaunchKernelGGL((ball_query_kernel<CP, CC, NW, PP, OT>), dim3((unsigned)nblk), dim3(64 * PP), \
-                           obytes, st, pp, cp_, (int)N, (int)S, (int)C, r2, (int)K, sm, out, cnt);     \
+        hipLaunchKernelGGL((ball_query_kernel<CP, CC, NW, PP, OT, RB>), dim3((unsigned)nblk),        \
+                           dim3(64 * PP), RB ? obytes : 0, st, pp, cp_, (int)N, (int)S, (int)C, r2,   \
+                           (int)K, sm, out, cnt);                                                      \
+    } while (0)
+#define PN2_BQ_L(NW, PP)                    \
+    do {                                    \
+        if (rowbuf) PN2_BQ_L2(NW, PP, true); \
+        else PN2_BQ_L2(NW, PP, false);       \
     } while (0)
     if (P == 8) {
         if (nw == 1) PN2_BQ_L(1, 8);
@@ -261,6 +284,7 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
         else PN2_BQ_L((CP > 4 ? 2 : 4), 16);
     }
 #undef PN2_BQ_L
+#undef PN2_BQ_L2
     PN2_LAUNCH_CHECK("ball_query_kernel");
     return PN2_OK;
 }

@@ -37,6 +37,8 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(compact_pool, 16)     /* LDS pool rows of compact chain launches (0: automatic)       */ \
     X(compact_stages, 3)   /* weight-ring stages of compact chain launches (2 or 3)        */ \
     X(bq_waves, 0)         /* ball query waves per workgroup (0: automatic, 8 or 16)       */ \
+    X(bq_rowbuf_kb, 96)    /* largest LDS row buffer of the ball query (KB); bigger rows   */ \
+                           /* are written straight to HBM (0: always)                      */ \
     X(fps_threads, 0)      /* FPS block shape threads x points per thread (0: automatic)   */ \
     X(fps_ppt, 0)                                                                              \
     X(dense_maxntc, 2)     /* widest 32-column tile count of the 4-wave dense layer         */ \

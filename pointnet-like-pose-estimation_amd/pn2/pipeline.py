@@ -348,6 +348,14 @@ def _clone(o):
     return o
 
 
+def _flat_tensors(o):
+    if isinstance(o, torch.Tensor):
+        return [o]
+    if isinstance(o, (tuple, list)):
+        return [t for x in o for t in _flat_tensors(x)]
+    return []
+
+
 # thread-local capture: other threads (the RCCL watchdog of a multi-GPU run) may keep querying
 # their own events while a pipeline slot is captured
 _MODE = "thread_local"
@@ -738,19 +746,20 @@ class GraphedPipeline(PipelinedForward):
                     # replay does not wait for the collective; a later batch of the group
                     # replaces it (same streams, later in their order)
                     ev_read[s].append(ts.record_event() if sl.tail_reads_geometry else ev_sa)
-                    if post is not None and ts in tails:
+                    if post is not None and ts is tail:
                         out = post(i, out)
                     ev_head[bs] = ts.record_event()
                     mark(i - first, "hd1", ts)
-                if post is not None and ts not in tails:
-                    # heads on the compute streams: `post` (e.g. the logits' all_gather) still
-                    # runs on one stream in batch order, so every rank's collectives execute in
-                    # the order they were issued
+                if post is not None and ts is not tail:
+                    # heads on a compute stream or on the second tail stream: `post` (e.g. the
+                    # logits' all_gather, or BatchedGather's stack of earlier batches' outputs)
+                    # still runs on one stream in batch order, so every rank's collectives
+                    # execute in the order they were issued and a bundle's outputs are all
+                    # complete on the stream that reads them
                     tail.wait_stream(ts)
                     with torch.cuda.stream(tail):
-                        for t in (out if isinstance(out, (tuple, list)) else (out,)):
-                            if isinstance(t, torch.Tensor):
-                                t.record_stream(tail)
+                        for t in _flat_tensors(out):
+                            t.record_stream(tail)
                         out = post(i, out)
                 outs.append(out)
                 top_up(-1, (g if h == gb - 1 else g - 1) + ng)

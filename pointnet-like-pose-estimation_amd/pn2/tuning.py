@@ -6,7 +6,7 @@ The product path reads one environment variable, once, at import:
 
 Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_set``:
 ``mlp_f32``, ``chain_prepass``, ``compact``, ``compact_pool``, ``compact_stages``,
-``bq_waves``, ``fps_threads``, ``fps_ppt``, ``dense_maxntc``, ``dense_minwg``,
+``bq_waves``, ``bq_rowbuf_kb``, ``fps_threads``, ``fps_ppt``, ``dense_maxntc``, ``dense_minwg``,
 ``dense_wide_minwg``) and these host-side ones:
 
     lib              path of an alternative libpn2.so build (A/B builds)

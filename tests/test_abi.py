@@ -85,7 +85,7 @@ def test_tuning_switch_keys():
     from pn2 import _lib, tuning
     L = _lib.load()
     keys = L.pn2_tuning_keys().decode().split()
-    for k in ("mlp_f32", "compact", "bq_waves", "fps_threads", "fps_ppt", "dense_lds"):
+    for k in ("mlp_f32", "compact", "bq_waves", "bq_rowbuf_kb", "fps_threads", "fps_ppt", "dense_lds"):
         assert k in keys
     v = ctypes.c_int64(-1)
     assert L.pn2_tuning_get(b"dense_lds", ctypes.byref(v)) == 0 and v.value == 0
