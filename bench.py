@@ -545,6 +545,9 @@ def main():
                            if not a.eager_pipeline else "")
                        if pipelined else "eager"),
             "eager_value": round(eager_value, 2),
+            # hardware queues of this process (bench.py sets 8 unless --hw-queues 0; HIP's own
+            # default is 4: DESIGN.md §6)
+            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default (4)"),
         }
         print(json.dumps(line))
     if world > 1:

@@ -65,8 +65,9 @@ const char *pn2_last_error(void);
 
 /* Device error word: conditions under which the reference raises but a kernel cannot.  The
  * kernels stay in bounds (clamped or NaN outputs, documented per entry point) and OR a bit into
- * a per-device word; pn2_device_errors reads it (synchronously: it waits for the device's
- * work) and clears it when `clear` != 0.  pn2.check_device_errors() raises IndexError.
+ * a per-device word; pn2_device_errors reads it (synchronously: hipDeviceSynchronize, so every
+ * stream's work is done) and, when `clear` != 0, clears it in the same device atomic (a bit
+ * raised meanwhile is never lost).  pn2.check_device_errors() raises IndexError.
  *   PN2_DEVERR_NO_NEIGHBOUR  a ball-query centroid had no point within the radius (its row is
  *                            padded with N, pointnet2_utils.py:85-89; the reference's next
  *                            index_points raises IndexError); the SA kernels read point 0 there
@@ -101,7 +102,7 @@ int64_t pn2_packed_stride(int64_t C);
  * C == 10, 4096 for other C (past that, up to N = 16384, the channels after xyz are re-read
  * from pts each iteration unless they are constant over the cloud: one-hot), with S <= 8192.
  * Any other N or S runs the streamed kernel: the points re-read every iteration, the running
- * distances in LDS up to N = 40952, past that in a caller workspace of
+ * distances in LDS up to N = 40896, past that in a caller workspace of
  * pn2_fps_workspace_bytes(B, N, C, S) bytes (pn2_fps_ws_f32; pn2_fps_f32 passes none and
  * fails with PN2_EINVAL when one is needed). */
 int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,

@@ -43,13 +43,20 @@ namespace pn2 {
 // raise IndexError); the SA kernels clamp such indices instead of reading past the cloud
 __device__ unsigned g_bq_errors;
 
+// the word's value (and, with clear, its reset) in ONE device atomic: a bit that a kernel ORs in
+// between cannot be lost (a read followed by a separate clear could drop it)
+__device__ unsigned g_bq_snapshot;
+__global__ void bq_errors_take_kernel(int clear) {
+    g_bq_snapshot = clear ? atomicExch(&g_bq_errors, 0u) : atomicOr(&g_bq_errors, 0u);
+}
+
 int read_bq_errors(unsigned *bits, int clear) {
+    // every stream's work first: kernels still in flight on other streams may raise bits
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    hipLaunchKernelGGL(bq_errors_take_kernel, dim3(1), dim3(1), 0, 0, clear);
+    if (hipGetLastError() != hipSuccess) return -1;
     unsigned v = 0;
-    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_bq_errors), sizeof(v)) != hipSuccess) return -1;
-    if (clear && v) {
-        const unsigned z = 0;
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bq_errors), &z, sizeof(z)) != hipSuccess) return -1;
-    }
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_bq_snapshot), sizeof(v)) != hipSuccess) return -1;
     *bits = v;
     return 0;
 }

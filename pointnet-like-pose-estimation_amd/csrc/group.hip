@@ -28,13 +28,20 @@ __device__ __forceinline__ int64_t torch_index(int64_t n, int64_t N) {
     return n;
 }
 
+// the word's value (and, with clear, its reset) in ONE device atomic: a bit that a kernel ORs in
+// between cannot be lost (a read followed by a separate clear could drop it)
+__device__ unsigned g_group_snapshot;
+__global__ void group_errors_take_kernel(int clear) {
+    g_group_snapshot = clear ? atomicExch(&g_group_errors, 0u) : atomicOr(&g_group_errors, 0u);
+}
+
 int read_group_errors(unsigned *bits, int clear) {
+    // every stream's work first: kernels still in flight on other streams may raise bits
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    hipLaunchKernelGGL(group_errors_take_kernel, dim3(1), dim3(1), 0, 0, clear);
+    if (hipGetLastError() != hipSuccess) return -1;
     unsigned v = 0;
-    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_group_errors), sizeof(v)) != hipSuccess) return -1;
-    if (clear && v) {
-        const unsigned z = 0;
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_group_errors), &z, sizeof(z)) != hipSuccess) return -1;
-    }
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_group_snapshot), sizeof(v)) != hipSuccess) return -1;
     *bits = v;
     return 0;
 }

@@ -136,7 +136,7 @@ def fps_direct(points: Tensor, npoint: int, start: Tensor) -> Tuple[Tensor, Tens
     ppk = torch.empty(B, N, cp, dtype=torch.float32, device=points.device)
     sb, sn, sc = points.stride()
     # past the register-resident shapes (N > 16384, npoint > 8192) the streamed kernel; past
-    # N = 40952 it keeps the running distances in this workspace
+    # N = 40896 it keeps the running distances in this workspace
     nws = int(_L.pn2_fps_workspace_bytes(B, N, C, npoint))
     ws = torch.empty(max(nws, 0) // 4, dtype=torch.float32, device=points.device) if nws > 0 else None
     _run("pn2_fps_f32", _L.pn2_fps_ws_f32,

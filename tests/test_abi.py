@@ -51,10 +51,13 @@ def test_workspace_queries_r03():
     from pn2 import _lib
     L = _lib.load()
     # FPS: register-resident shapes and the streamed kernel with LDS distances need none; past
-    # N = 40952 one word per point
+    # N = 40896 one word per point
     assert L.pn2_fps_workspace_bytes(4, 16384, 3, 512) == 0
     assert L.pn2_fps_workspace_bytes(4, 32768, 3, 512) == 0
     assert L.pn2_fps_workspace_bytes(4, 50000, 3, 256) == 4 * 50000 * 4
+    # the LDS holds the 16 double-buffered 8-byte wave slots beside the N words
+    assert L.pn2_fps_workspace_bytes(2, 40896, 3, 256) == 0
+    assert L.pn2_fps_workspace_bytes(2, 40897, 3, 256) == 2 * 40897 * 4
     assert L.pn2_fps_workspace_bytes(0, 0, 3, 1) == -1
     # the FC tail: y1 and y2, each padded to 4 floats
     assert L.pn2_fc_tail_workspace_bytes(32, 512, 256) == (32 * 512 + 32 * 256) * 4
@@ -68,7 +71,7 @@ def test_validation_errors_r03_without_gpu():
     # int32 ball query: the same shape checks as the int64 one
     rc = L.pn2_ball_query_i32(1, 1, 2, 8, 4, 3, 0.2, 9, 1, None, None)
     assert rc == -1 and b"sample_number 9 > N 8" in L.pn2_last_error()
-    # streamed FPS past N = 40952 without the workspace it needs
+    # streamed FPS past N = 40896 without the workspace it needs
     rc = L.pn2_fps_ws_f32(1, 2, 50000, 3, 150000, 3, 1, 1, 16, 1, None, None, None, None, 0, None)
     assert rc == -1 and b"workspace" in L.pn2_last_error()
     rc = L.pn2_fps_f32(1, 2, 50000, 3, 150000, 3, 1, 1, 16, 1, None, None, None, None)
