@@ -236,6 +236,27 @@ def load_traffic(cfg, op="pn2_sa_mlp_max_f32"):
         return None
 
 
+def load_mfma_busy(cfg):
+    """MFMA-pipe busy fraction of the MLP op's kernels from the SQ counters
+    (profiles/sq_mfma.json, tools/sq_mfma.sh: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x
+    1024 SIMDs), each kernel alone on the chip): per kernel, and time-weighted over them --
+    the executed-products fraction of the MFMA peak beside roofline.frac's algorithmic one."""
+    p = os.path.join(ROOT, "profiles", "sq_mfma.json")
+    try:
+        with open(p) as fh:
+            d = json.load(fh).get(cfg, {})
+    except (OSError, ValueError):
+        return None
+    mlp = {k: v for k, v in d.items() if "sa_chain_kernel" in k or "dense_split_kernel" in k}
+    if not mlp:
+        return None
+    t = sum(v["gui_us"] * v["calls"] for v in mlp.values())
+    agg = sum(v["mfma_busy"] * v["gui_us"] * v["calls"] for v in mlp.values()) / t
+    short = {k.split("(")[0].replace("void pn2::", ""): v["mfma_busy"] for k, v in mlp.items()}
+    return {"time_weighted": round(agg, 4), "per_kernel": short,
+            "source": "profiles/sq_mfma.json (SQ_VALU_MFMA_BUSY_CYCLES, eager launch)"}
+
+
 def count_gpus(topology="/sys/class/kfd/kfd/topology/nodes"):
     """GPUs this process may use, counted without initialising HIP: the KFD topology's GPU
     nodes (simd_count > 0), capped by HIP_/ROCR_/CUDA_VISIBLE_DEVICES.  The launcher's parent
@@ -489,6 +510,7 @@ def main():
                                "only each group's distinct neighbour rows), so achieved and "
                                "frac are effective rates",
                 "avg_launch_ms": mlp["ms"] / mlp["launches"]}
+        roof["mfma_busy"] = load_mfma_busy(a.config)
         if roof["traffic"]:
             roof["traffic_vs_compulsory"] = round(roof["traffic"] / roof["compulsory_bytes_per_launch"], 2)
     kernels = {k: {"ms_per_step": round(v["ms"] / a.steps, 4), "launches_per_step": v["launches"] / a.steps}

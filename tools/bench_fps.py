@@ -42,11 +42,19 @@ def main():
         sd = start.to(dev)
         want = oracle.farthest_point_sample(x[:2], S, start[:2])
         only = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--variants=")]
-        for v in (only[0] if only else [""] if only_default else VARIANTS):
+        culls = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--cull=")]
+        todo = [(v, 1) for v in (only[0] if only else [""] if only_default else VARIANTS)]
+        if culls:  # fps_cull values (0: index-ordered kernel, 1: default culled shape, NT*100+Q*10+PPC)
+            todo = [("", int(cv)) for cv in culls[0]]
+        for v, cull in todo:
             nt, ppt = map(int, v.split("x")) if v else (0, 0)
             if v and (nt * ppt < N or (nt * ppt >= 4 * N and not only)):
                 continue
-            with tuning.override(fps_threads=nt, fps_ppt=ppt):
+            if cull > 1 and (cull // 100) * ((cull // 10) % 10) * (cull % 10) < N:
+                continue
+            if v == "" and cull != 1:
+                v = "cull=%d" % cull
+            with tuning.override(fps_threads=nt, fps_ppt=ppt, fps_cull=cull):
                 idx = torch.ops.pn2.fps(xd, S, sd)[0]
                 ok = bool((idx[:2].cpu().numpy() == want).all())
                 torch.cuda.synchronize()

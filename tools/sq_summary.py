@@ -5,7 +5,15 @@ mfma_busy = it / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs)."""
 import collections
 import csv
 import glob
+import json
 import sys
+
+# --json PATH: also write {kernel: {mfma_busy, gui_us, calls}} (bench.py's roofline.mfma_busy)
+jpath = None
+if "--json" in sys.argv:
+    i = sys.argv.index("--json")
+    jpath = sys.argv[i + 1]
+    del sys.argv[i:i + 2]
 
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.defaultdict(collections.Counter)
@@ -38,3 +46,13 @@ for gui, k, c, waves, wc in rows[:25]:
         c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1, c.get("SQ_LDS_IDX_ACTIVE", 0)),
         # LDS-array cycles per CU-cycle of the kernel (256 CUs): the LDS's busy fraction
         "%.3f" % (lact / (gui / 8 * 256)) if lact and gui else "-"))
+
+if jpath:
+    out = {}
+    for gui, k, c, waves, wc in rows:
+        mf = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
+        if mf and gui:
+            out[k] = {"mfma_busy": round(mf / (gui / 8 * 1024), 4), "gui_us": round(gui / 8 / 2.4e3, 2),
+                      "calls": int(calls[k]["GRBM_GUI_ACTIVE"])}
+    with open(jpath, "w") as fh:
+        json.dump(out, fh, indent=1, sort_keys=True)
