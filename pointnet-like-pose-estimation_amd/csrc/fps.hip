@@ -544,15 +544,32 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
     // that point's place in the chunk
     unsigned cm[Q], cb[Q];
     int ci[Q];
-    auto chunk_best = [&](int q) {
-        unsigned pi[PPC];
-        if constexpr (PPC == 4) {
+    // point indices of the lane's chunks: registers for small PPT, else read from perm (LDS)
+    // at the start of an active chunk's update, before its distance math
+    constexpr bool IDXREG = PPT <= 8;
+    unsigned preg[IDXREG ? PPT : 1];
+    if constexpr (IDXREG) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+#pragma unroll
+            for (int i = 0; i < PPC; ++i) preg[q * PPC + i] = (unsigned)myperm[q * CS + i];
+    }
+    auto chunk_idx = [&](int q, unsigned (&pi)[PPC]) {
+        if constexpr (IDXREG) {
+#pragma unroll
+            for (int i = 0; i < PPC; ++i) pi[i] = preg[q * PPC + i];
+        } else if constexpr (PPC == 4) {
             const int4 v = *reinterpret_cast<const int4 *>(myperm + q * CS);
             pi[0] = v.x; pi[1] = v.y; pi[2] = v.z; pi[3] = v.w;
+        } else if constexpr (PPC == 2) {
+            const int2 v = *reinterpret_cast<const int2 *>(myperm + q * CS);
+            pi[0] = v.x; pi[1] = v.y;
         } else {
 #pragma unroll
             for (int i = 0; i < PPC; ++i) pi[i] = (unsigned)myperm[q * CS + i];
         }
+    };
+    auto chunk_best = [&](int q, const unsigned (&pi)[PPC]) {
         unsigned m = dist[q * PPC];
 #pragma unroll
         for (int i = 1; i < PPC; ++i) m = max(m, dist[q * PPC + i]);
@@ -569,7 +586,11 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
         ci[q] = bii;
     };
 #pragma unroll
-    for (int q = 0; q < Q; ++q) chunk_best(q);
+    for (int q = 0; q < Q; ++q) {
+        unsigned pi[PPC];
+        chunk_idx(q, pi);
+        chunk_best(q, pi);
+    }
 
     // the wave's candidate: its maximum, the smallest index at it, and (!LDSC) its coordinates
     unsigned wv = 0, wi = 0x7FFFFFFFu;
@@ -608,7 +629,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
     float c[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) c[k] = P[(int64_t)far * sn + (int64_t)k * sc];
-    if (LDSC && tid < 3) key[tid] = 0ull;
+    if (tid < 3) key[tid] = 0ull;
     __syncthreads();
 
     for (int it = 0;; ++it) {
@@ -641,6 +662,8 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 if (act & (1u << q)) {
+                    unsigned pi[PPC];
+                    chunk_idx(q, pi);  // (LDS: in flight during the distance math)
 #pragma unroll
                     for (int h = 0; h < PPC / 2; ++h) {
                         const int j = q * PPC + 2 * h;
@@ -654,7 +677,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
                         dist[j] = min(dist[j], __float_as_uint(dd.x));
                         dist[j + 1] = min(dist[j + 1], __float_as_uint(dd.y));
                     }
-                    chunk_best(q);
+                    chunk_best(q, pi);
                 }
             }
             wave_best();
@@ -669,30 +692,23 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
             c[1] = r4.y;
             c[2] = r4.z;
         } else {
+            // the same 64-bit key max; each wave's candidate coordinates (and index) sit in its
+            // slot (double-buffered by parity), read by lanes 0..NW-1 beside the key
             const int par = it & 1;
             if (lane == 0) {
-                float4 *sl = reinterpret_cast<float4 *>(slots + (par * NW + wave) * 8);
-                sl[0] = float4{__uint_as_float(wv), __uint_as_float(wi), wc[0], wc[1]};
-                sl[1] = float4{wc[2], 0.f, 0.f, 0.f};
+                atomicMax(&key[it % 3], ((unsigned long long)wv << 32) | (0xFFFFFFFFu - wi));
+                reinterpret_cast<float4 *>(slots)[par * NW + wave] = float4{wc[0], wc[1], wc[2], __uint_as_float(wi)};
             }
+            if (tid == 64) key[(it + 1) % 3] = 0ull;
             __syncthreads();
-            unsigned rv = 0u, ri = 0xFFFFFFFFu;
-            float rc[3] = {0.f, 0.f, 0.f};
-            if (lane < NW) {
-                const float4 *sl = reinterpret_cast<const float4 *>(slots + (par * NW + lane) * 8);
-                const float4 a = sl[0], e = sl[1];
-                rv = __float_as_uint(a.x);
-                ri = __float_as_uint(a.y);
-                rc[0] = a.z;
-                rc[1] = a.w;
-                rc[2] = e.x;
-            }
-            const unsigned gv = __builtin_amdgcn_readlane(row_max_u32(rv), 0);
-            const unsigned gi = ~__builtin_amdgcn_readlane(row_max_u32(rv == gv ? ~ri : 0u), 0);
-            const int gw = (int)__builtin_ctzll(__ballot(lane < NW && rv == gv && ri == gi));
-            far = (int)gi;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rc[k]), gw));
+            const unsigned kw = (unsigned)key[it % 3];
+            float4 sv = {0.f, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)};
+            if (lane < NW) sv = reinterpret_cast<const float4 *>(slots)[par * NW + lane];
+            far = __builtin_amdgcn_readfirstlane((int)(0xFFFFFFFFu - kw));
+            const int gw = (int)__builtin_ctzll(__ballot(lane < NW && __float_as_uint(sv.w) == (unsigned)far));
+            c[0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv.x), gw));
+            c[1] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv.y), gw));
+            c[2] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv.z), gw));
         }
     }
     __syncthreads();

@@ -100,6 +100,22 @@ __device__ unsigned long long g_chain_stamps[kStampWG * kStamps];
 constexpr int kUnitRows = 8;
 constexpr int kUnitsPerWG = kChainRows / kUnitRows;  // 16
 
+// Pool merges.  HBM: a global_atomic_umax through a global (not generic) pointer -- a flat
+// atomic counts in both vmcnt and lgkmcnt and the compiler drained vmcnt(0) (the weight ring's
+// copies in flight) before each one.  LDS: ds_max_u32 as inline asm -- as a C++ atomic the
+// compiler waited for every LDS-DMA copy in flight (vmcnt(0)) first, since the ring's copies
+// write the same dynamic LDS array; the pool never overlaps the ring, and its readers sit
+// behind a barrier with lgkmcnt(0).
+__device__ __forceinline__ void hbm_max_u32(float *p, unsigned v) {
+    __hip_atomic_fetch_max(reinterpret_cast<__attribute__((address_space(1))) unsigned *>(
+                               reinterpret_cast<uintptr_t>(p)),
+                           v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lds_max_u32(unsigned *p, unsigned v) {
+    const unsigned a = (unsigned)(size_t)(__attribute__((address_space(3))) unsigned *)p;
+    asm volatile("ds_max_u32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
 template <int NP>
 __device__ __forceinline__ Split load_w(const ChainLayer &L, int t, int kb, int lane) {
     const int64_t plane = (int64_t)L.tiles * L.kb * 64;
@@ -281,6 +297,123 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     // groups per workgroup of the LDS pool (pool_mode 1; compact: up to one per unit)
     const int gpb = compact ? A.pool_rows : kChainRows / A.K;
 
+    // ---- prologue.  vmcnt counts in issue order (a wait for one load waits for every older
+    // one), so the independent loads go out oldest-first in the order they are needed: the BN
+    // operands (registers, written to LDS below), the first weight-ring stages (they land while
+    // the dependent row gather runs, instead of after the setup barrier), then the gather.
+    float *bn = reinterpret_cast<float *>(csm + A.lds_bn);
+    float *al0 = bn, *be0 = al0 + 32 * T0, *al1 = be0 + 32 * T0, *be1 = al1 + 32 * T1;
+    float *al2 = be1 + 32 * T1, *be2 = al2 + coutL;
+    const bool bnreg = coutL <= 2 * 64 * kChainWaves;  // every thread's share fits 8 registers
+    float bnv[8];
+    if (bnreg) {
+        const int e2 = tid + 64 * kChainWaves;
+        bnv[0] = tid < 32 * T0 ? L0.alpha[tid] : 0.f;
+        bnv[1] = tid < 32 * T0 ? L0.beta[tid] : 0.f;
+        bnv[2] = tid < 32 * T1 ? L1.alpha[tid] : 0.f;
+        bnv[3] = tid < 32 * T1 ? L1.beta[tid] : 0.f;
+        bnv[4] = tid < coutL ? L2.alpha[tid] : 0.f;
+        bnv[5] = tid < coutL ? L2.beta[tid] : 0.f;
+        bnv[6] = e2 < coutL ? L2.alpha[e2] : 0.f;
+        bnv[7] = e2 < coutL ? L2.beta[e2] : 0.f;
+    }
+
+    char *ring = csm + A.lds_ring;
+    const unsigned loff = (unsigned)lane * 16u;
+    // Ring steps in consumption order: layers 0 (resident input only) and 1 block-major, layer 2
+    // tile-major; source addresses come from scalar arithmetic on the layer's base.
+    auto issue_l = [&](const ChainLayer &L, int t, int kb, char *dst) {
+        ring_issue<NP>(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64, dst, loff);
+    };
+    auto issue2 = [&](int z, char *dst) {  // layer-2 step z
+        z = min(z, L2.tiles * KB2 - 1);
+        issue_l(L2, z / KB2, z % KB2, dst);
+    };
+    auto issue1 = [&](int y, char *dst) {  // layer-1 step y (block-major)
+        if (y < T1 * KB1) issue_l(L1, y % T1, y / T1, dst);
+        else issue2(y - T1 * KB1, dst);
+    };
+    const int n0 = T0 * L0.kb;
+    auto issue_stage = [&](int st) {  // this wave's step of stage st
+        const int x = st * kChainWaves + wave;
+        char *dst = ring + (st % KS) * kStageBytes + wave * kStepBytes;
+        if constexpr (KB0M > 0) {
+            if (x < n0) issue_l(L0, x % T0, x / T0, dst);
+            else issue1(x - n0, dst);
+        } else {
+            issue1(x, dst);
+        }
+    };
+    int nread = 0;
+    auto read_w = [&]() {
+        if ((nread & (kChainWaves - 1)) == 0) {  // first step of a stage
+            const int st = nread / kChainWaves;
+            ring_fence();
+            stage_wait<NP, KS>();
+            stage_barrier();
+            issue_stage(st + KS - 1);
+        }
+        const Split w = ring_readN<NP>(ring + ((nread / kChainWaves) % KS) * kStageBytes +
+                                      (nread & (kChainWaves - 1)) * kStepBytes, lane);
+        ++nread;
+        return w;
+    };
+    // One step of lookahead: the next step's weight planes are read before this step's MFMAs
+    // (the compiler kept two fragments in flight and waited lgkmcnt(0) every 2-3 MFMAs: an LDS
+    // round trip exposed per step, ISA of sa_chain_kernel<4,4,-1>).  The last step reads one
+    // step past the end, unconditionally: a branch there made every step's MFMAs a control-flow
+    // merge, where the compiler waited for the lookahead reads as well (lgkmcnt(0)).  The ring
+    // repeats its last step past the end, so that read is in bounds; it is never used.
+    Split wpre;
+    bool primed = false;
+    auto next_w = [&]() {
+        if (!primed) {
+            wpre = read_w();
+            primed = true;
+        }
+        const Split w = wpre;
+        wpre = read_w();
+        return w;
+    };
+    // ASMR (split chains with a register-resident or pre-transformed layer 0): the weight
+    // planes are read by inline-asm ds_read_b128 into two register sets used alternately, the
+    // next step's reads issued before this step's MFMAs, and each step waits for its own reads
+    // only (lgkmcnt(3): the next step's three reads may stay in flight).  The compiler's own
+    // schedule kept one or two fragments in flight and waited lgkmcnt(0) before most MFMAs
+    // (register pressure, and the stage-sync branch merges).  Pending asm reads never cross a
+    // control-flow merge: the runtime tile loop of layer 2 waits lgkmcnt(0) before its back-edge.
+#ifndef PN2_CHAIN_ASMR
+#define PN2_CHAIN_ASMR 1
+#endif
+    constexpr bool ASMR = PN2_CHAIN_ASMR && NP == 3 && (KB0M == 1 || KB0M < 0);
+    Split WB[2];
+    int nr = 0;  // ASMR: the next step to read
+    const unsigned ring3 = (unsigned)(size_t)(__attribute__((address_space(3))) char *)ring;
+    auto rd = [&](Split &w) {
+        if ((nr & (kChainWaves - 1)) == 0) {  // first step of a stage: see read_w
+            ring_fence();
+            stage_wait<NP, KS>();
+            stage_barrier();
+            issue_stage(nr / kChainWaves + KS - 1);
+        }
+        const unsigned a = ring3 + (unsigned)(((nr / kChainWaves) % KS) * kStageBytes +
+                                              (nr & (kChainWaves - 1)) * kStepBytes) + loff;
+        asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:1024\n\tds_read_b128 %2, %3 offset:2048"
+                     : "=&v"(w.h), "=&v"(w.m), "=&v"(w.l)
+                     : "v"(a));
+        ++nr;
+    };
+    auto wt3 = [&](Split &w) { asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(w.h), "+v"(w.m), "+v"(w.l)); };
+    auto wt0 = [&](Split &w) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w.h), "+v"(w.m), "+v"(w.l)); };
+    constexpr int P0 = KB0M > 0 ? T0 * KB0M : 0;  // ASMR layer-0 steps (L0.kb == KB0M == 1)
+    constexpr int P1 = P0 + T1 * KB1;              // steps before layer 2
+
+    if constexpr (KB0M != 0) {  // KB0M == 0: the ring starts after layer 0's streamed loads
+#pragma unroll
+        for (int st = 0; st < KS - 1; ++st) issue_stage(st);
+    }
+
+
     // ---- this lane's row: (group g, batch b, point n)
     unsigned g;
     bool valid;
@@ -364,64 +497,28 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
     }
 
-    // stage BN scale/shift of the three layers: [al0|be0|al1|be1|al2|be2]
-    float *bn = reinterpret_cast<float *>(csm + A.lds_bn);
-    float *al0 = bn, *be0 = al0 + 32 * T0, *al1 = be0 + 32 * T0, *be1 = al1 + 32 * T1;
-    float *al2 = be1 + 32 * T1, *be2 = al2 + coutL;
-    for (int e = tid; e < 32 * T0; e += 64 * kChainWaves) { al0[e] = L0.alpha[e]; be0[e] = L0.beta[e]; }
-    for (int e = tid; e < 32 * T1; e += 64 * kChainWaves) { al1[e] = L1.alpha[e]; be1[e] = L1.beta[e]; }
-    for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
+    // BN operands to LDS, the pool zeroed; no vmcnt drain at the barrier: the gather and the
+    // ring's first stages stay in flight (their consumers wait for them)
+    if (bnreg) {
+        const int e2 = tid + 64 * kChainWaves;
+        if (tid < 32 * T0) { al0[tid] = bnv[0]; be0[tid] = bnv[1]; }
+        if (tid < 32 * T1) { al1[tid] = bnv[2]; be1[tid] = bnv[3]; }
+        if (tid < coutL) { al2[tid] = bnv[4]; be2[tid] = bnv[5]; }
+        if (e2 < coutL) { al2[e2] = bnv[6]; be2[e2] = bnv[7]; }
+    } else {
+        for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
+        for (int e = tid; e < 32 * T0; e += 64 * kChainWaves) { al0[e] = L0.alpha[e]; be0[e] = L0.beta[e]; }
+        for (int e = tid; e < 32 * T1; e += 64 * kChainWaves) { al1[e] = L1.alpha[e]; be1[e] = L1.beta[e]; }
+    }
     if (A.pool_mode == 1 || compact)
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stage_barrier();
     PN2_STAMP(1);
-    char *ring = csm + A.lds_ring;
-    const unsigned loff = (unsigned)lane * 16u;
-    // Ring steps in consumption order: layers 0 (resident input only) and 1 block-major, layer 2
-    // tile-major; source addresses come from scalar arithmetic on the layer's base.
-    auto issue_l = [&](const ChainLayer &L, int t, int kb, char *dst) {
-        ring_issue<NP>(L.w + ((int64_t)t * L.kb + kb) * 64, (int64_t)L.tiles * L.kb * 64, dst, loff);
-    };
-    auto issue2 = [&](int z, char *dst) {  // layer-2 step z
-        z = min(z, L2.tiles * KB2 - 1);
-        issue_l(L2, z / KB2, z % KB2, dst);
-    };
-    auto issue1 = [&](int y, char *dst) {  // layer-1 step y (block-major)
-        if (y < T1 * KB1) issue_l(L1, y % T1, y / T1, dst);
-        else issue2(y - T1 * KB1, dst);
-    };
-    const int n0 = T0 * L0.kb;
-    auto issue_stage = [&](int st) {  // this wave's step of stage st
-        const int x = st * kChainWaves + wave;
-        char *dst = ring + (st % KS) * kStageBytes + wave * kStepBytes;
-        if constexpr (KB0M > 0) {
-            if (x < n0) issue_l(L0, x % T0, x / T0, dst);
-            else issue1(x - n0, dst);
-        } else {
-            issue1(x, dst);
-        }
-    };
-    int nread = 0;
-    auto read_w = [&]() {
-        if ((nread & (kChainWaves - 1)) == 0) {  // first step of a stage
-            const int st = nread / kChainWaves;
-            ring_fence();
-            stage_wait<NP, KS>();
-            stage_barrier();
-            issue_stage(st + KS - 1);
-        }
-        const Split w = ring_readN<NP>(ring + ((nread / kChainWaves) % KS) * kStageBytes +
-                                      (nread & (kChainWaves - 1)) * kStepBytes, lane);
-        ++nread;
-        return w;
-    };
-
     typename HidT<NP>::type X1[2 * T0];
     if constexpr (KB0M < 0) {
         // ---- layer 0 pre-transformed: acc = z[point] - u[group], already in the transposed
         // accumulator layout (register 4m + i of lane (r, h) = channel 32t + 8m + 4h + i)
-#pragma unroll
-        for (int st = 0; st < KS - 1; ++st) issue_stage(st);
         const float *zrow = A.z + ((int64_t)b * s.N + n) * (32 * T0);
         const float *urow = A.u + (int64_t)g * (32 * T0);
         // Tile t+1's z / u loads are issued while tile t is split (one tile of lookahead).  The
@@ -463,20 +560,29 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     } else if constexpr (KB0M > 0) {
         // ---- layer 0 from registers: the whole input gathered once (raw fp32), then k-outer
         // (each block split once, every output tile accumulating) with weights from the ring
-        auto &x = x0;  // gathered before the setup
-#pragma unroll
-        for (int st = 0; st < KS - 1; ++st) issue_stage(st);  // overlaps the gather's latency
+        auto &x = x0;  // gathered before the setup; the ring's first stages are in flight
         cfloatx16 acc[T0];
 #pragma unroll
         for (int t = 0; t < T0; ++t)
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+        if constexpr (ASMR) {  // KB0M == 1: one block, T0 steps
+            rd(WB[0]);
+            const Split xs = splitN<NP>(x[0]);
 #pragma unroll
-        for (int kb = 0; kb < KB0M; ++kb) {
-            if (kb < L0.kb) {
-                const Split xs = splitN<NP>(x[kb]);
+            for (int t = 0; t < T0; ++t) {
+                rd(WB[(t + 1) & 1]);
+                wt3(WB[t & 1]);
+                acc[t] = mma_wa<NP>(WB[t & 1], xs, acc[t]);
+            }
+        } else {
 #pragma unroll
-                for (int t = 0; t < T0; ++t) acc[t] = mma_wa<NP>(read_w(), xs, acc[t]);
+            for (int kb = 0; kb < KB0M; ++kb) {
+                if (kb < L0.kb) {
+                    const Split xs = splitN<NP>(x[kb]);
+#pragma unroll
+                    for (int t = 0; t < T0; ++t) acc[t] = mma_wa<NP>(next_w(), xs, acc[t]);
+                }
             }
         }
 #pragma unroll
@@ -523,11 +629,28 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         for (int t = 0; t < T1; ++t)
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+        if constexpr (ASMR) {
+            if constexpr (KB0M < 0) rd(WB[0]);  // (KB0M == 1: layer 0 read this step ahead)
 #pragma unroll
-        for (int kb = 0; kb < KB1; ++kb) {
-            const Split xs = hid_split<NP>(X1[kb]);
+            for (int kb = 0; kb < KB1; ++kb) {
+                const Split xs = hid_split<NP>(X1[kb]);
 #pragma unroll
-            for (int t = 0; t < T1; ++t) acc[t] = mma_wa<NP>(read_w(), xs, acc[t]);
+                for (int t = 0; t < T1; ++t) {
+                    constexpr int dummy = 0;
+                    (void)dummy;
+                    const int g = P0 + kb * T1 + t;  // compile-time after unrolling
+                    rd(WB[(g + 1) & 1]);
+                    wt3(WB[g & 1]);
+                    acc[t] = mma_wa<NP>(WB[g & 1], xs, acc[t]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int kb = 0; kb < KB1; ++kb) {
+                const Split xs = hid_split<NP>(X1[kb]);
+#pragma unroll
+                for (int t = 0; t < T1; ++t) acc[t] = mma_wa<NP>(next_w(), xs, acc[t]);
+            }
         }
 #pragma unroll
         for (int t = 0; t < T1; ++t) hidden_epilogue<NP>(acc[t], al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
@@ -540,8 +663,18 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         cfloatx16 acc;
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+        if constexpr (ASMR) {
 #pragma unroll
-        for (int kb = 0; kb < KB2; ++kb) acc = mma_wb<NP>(X2[kb], read_w(), acc);
+            for (int kb = 0; kb < KB2; ++kb) {
+                const int b = (P1 + kb) & 1;  // KB2 is even: the same parity in every tile
+                rd(WB[b ^ 1]);                // kb = KB2 - 1: the next tile's first step
+                wt3(WB[b]);
+                acc = mma_wb<NP>(X2[kb], WB[b], acc);
+            }
+        } else {
+#pragma unroll
+            for (int kb = 0; kb < KB2; ++kb) acc = mma_wb<NP>(X2[kb], next_w(), acc);
+        }
         // max over rows of relu(fma(acc, al, be)) = relu(fma(extreme, al, be)) exactly: fma with
         // a fixed al is monotone in acc (non-decreasing for al >= 0, else non-increasing) and
         // so is relu -- only the row max (al >= 0) or min of the accumulator is needed.
@@ -560,10 +693,10 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             auto flush = [&]() {
                 if (sg >= 0 && h == 0) {
                     if (sg < gpb)
-                        atomicMax(&cpool[sg * coutL + col], __float_as_uint(fin(smx, smn)));
+                        lds_max_u32(&cpool[sg * coutL + col], __float_as_uint(fin(smx, smn)));
                     else  // past the pool (rare): the row was zeroed by the scan
-                        atomicMax(reinterpret_cast<unsigned *>(A.out + (int64_t)(c_g0 + (unsigned)sg) * A.ostride + col),
-                                  __float_as_uint(fin(smx, smn)));
+                        hbm_max_u32(A.out + (int64_t)(c_g0 + (unsigned)sg) * A.ostride + col,
+                                    __float_as_uint(fin(smx, smn)));
                 }
             };
 #pragma unroll
@@ -623,11 +756,14 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             if (h == 0 && (unsigned)slab * 32u < (unsigned)A.M) {
                 if (A.pool_mode == 0) A.out[(int64_t)gg * A.ostride + col] = m;
                 else if (A.pool_mode == 1)
-                    atomicMax(&cpool[(int)(gg - (unsigned)bid * gpb) * coutL + col], __float_as_uint(m));
+                    lds_max_u32(&cpool[(int)(gg - (unsigned)bid * gpb) * coutL + col], __float_as_uint(m));
                 else
-                    atomicMax(reinterpret_cast<unsigned *>(A.out + (int64_t)gg * A.ostride + col), __float_as_uint(m));
+                    hbm_max_u32(A.out + (int64_t)gg * A.ostride + col, __float_as_uint(m));
             }
         }
+        // ASMR: the next tile's first weights (read under this tile's last MFMAs and its
+        // epilogue) have landed before the loop's back-edge
+        if constexpr (ASMR) wt0(WB[P1 & 1]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing (repeat) copies
     PN2_STAMP(4);
@@ -639,7 +775,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             const int gl = e / coutL, c = e - gl * coutL;
             float *o = A.out + (int64_t)(c_g0 + (unsigned)gl) * A.ostride + c;
             if ((gl == 0 && (c_flags & 1)) || (gl == c_ng - 1 && (c_flags & 2)))
-                atomicMax(reinterpret_cast<unsigned *>(o), cpool[e]);
+                hbm_max_u32(o, cpool[e]);
             else
                 *o = __uint_as_float(cpool[e]);
         }
