@@ -317,6 +317,22 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
 // Diagnostic builds only (tools/debug/fps_cull_stats.py): -DPN2_FPS_STATS counts active chunks
 // per (wave, iteration); -DPN2_FPS_FLOOR skips every chunk after the first iteration (wrong
 // indices: the loop's fixed cost alone).
+#ifdef PN2_FPS_STAMPS
+// per (iteration < 128, wave < 16, point < 4) s_memtime of cloud 0: loop top, after the
+// activity test, after the chunk updates + wave candidate, after the barrier
+__device__ unsigned long long g_fps_stamps[128 * 16 * 4];
+extern "C" int pn2_debug_fps_stamps(unsigned long long *out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fps_stamps), sizeof(g_fps_stamps)) == hipSuccess ? 0 : -1;
+}
+#define PN2_FPS_STAMP(k)                                                                        \
+    do {                                                                                       \
+        if (b == 0 && lane == 0 && it < 128)                                                   \
+            g_fps_stamps[(it * 16 + wave) * 4 + (k)] = __builtin_amdgcn_s_memtime();           \
+    } while (0)
+#else
+#define PN2_FPS_STAMP(k) do {} while (0)
+#endif
 #ifdef PN2_FPS_STATS
 __device__ unsigned long long g_fps_stats[4];
 extern "C" int pn2_debug_fps_stats(unsigned long long *out, int clear) {
@@ -332,8 +348,8 @@ extern "C" int pn2_debug_fps_stats(unsigned long long *out, int clear) {
 // The same serial loop with spatial ownership and exact culling.  In the prologue the cloud is
 // sorted into a Morton order of a coarse grid over its bounding box (a counting sort in LDS:
 // cell ranks by LDS atomics, a block scan, a scatter of the point indices); the sorted order is
-// cut into chunks of 64*PPC points, Q chunks per wave, and lane l holds PPC points of each of its
-// wave's chunks (registers, as above).  Each chunk is a compact region with a bounding box.
+// cut into chunks of 64*PPC points, Q chunks per wave (chunk q of wave w is sorted chunk
+// q*NW + w), and lane l holds PPC points of each of its wave's chunks (registers, as above).  Each chunk is a compact region with a bounding box.
 //
 // Culling is exact.  For a centroid c and a box [lo, hi], q = clamp(c, lo, hi) is one of c, lo,
 // hi per channel, and LB = ((fl(qx-cx)^2 + fl(qy-cy)^2) + fl(qz-cz)^2) -- the reference's own
@@ -490,20 +506,23 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
     }
     __syncthreads();
 
-    // ---- pass D: this lane's points: chunk q of wave w = sorted positions (wQ + q) * CS ..,
+    // ---- pass D: this lane's points: chunk q of wave w = sorted positions (qNW + w) * CS ..,
     // lane l takes PPC consecutive ones (their indices stay in LDS: perm).  Per channel one
     // register vector, so a wave-uniform register index picks a point's coordinates.
     typedef float VQ __attribute__((ext_vector_type(PPT)));
     VQ X[3];
     unsigned dist[PPT];
-    const int *myperm = perm + wave * Q * CS + lane * PPC;  // + q * CS + i
+    // chunk q of wave w is sorted chunk q * NW + w: neighbouring chunks (in Morton order) sit
+    // in different waves, so the few chunks near a new centroid are updated in parallel on
+    // several SIMDs rather than one after another by one wave
+    const int *myperm = perm + wave * CS + lane * PPC;  // + q * NW * CS + i
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
 #pragma unroll
         for (int i = 0; i < PPC; ++i) {
             const int j = q * PPC + i;
-            const int s = (wave * Q + q) * CS + lane * PPC + i;
-            const int n = s < N ? myperm[q * CS + i] : -1;
+            const int s = (q * NW + wave) * CS + lane * PPC + i;
+            const int n = s < N ? myperm[q * NW * CS + i] : -1;
             dist[j] = n >= 0 ? __float_as_uint(1e10f) : 0u;  // padding: 0, never the maximum's first index
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
@@ -552,21 +571,21 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
 #pragma unroll
         for (int q = 0; q < Q; ++q)
 #pragma unroll
-            for (int i = 0; i < PPC; ++i) preg[q * PPC + i] = (unsigned)myperm[q * CS + i];
+            for (int i = 0; i < PPC; ++i) preg[q * PPC + i] = (unsigned)myperm[q * NW * CS + i];
     }
     auto chunk_idx = [&](int q, unsigned (&pi)[PPC]) {
         if constexpr (IDXREG) {
 #pragma unroll
             for (int i = 0; i < PPC; ++i) pi[i] = preg[q * PPC + i];
         } else if constexpr (PPC == 4) {
-            const int4 v = *reinterpret_cast<const int4 *>(myperm + q * CS);
+            const int4 v = *reinterpret_cast<const int4 *>(myperm + q * NW * CS);
             pi[0] = v.x; pi[1] = v.y; pi[2] = v.z; pi[3] = v.w;
         } else if constexpr (PPC == 2) {
-            const int2 v = *reinterpret_cast<const int2 *>(myperm + q * CS);
+            const int2 v = *reinterpret_cast<const int2 *>(myperm + q * NW * CS);
             pi[0] = v.x; pi[1] = v.y;
         } else {
 #pragma unroll
-            for (int i = 0; i < PPC; ++i) pi[i] = (unsigned)myperm[q * CS + i];
+            for (int i = 0; i < PPC; ++i) pi[i] = (unsigned)myperm[q * NW * CS + i];
         }
     };
     auto chunk_best = [&](int q, const unsigned (&pi)[PPC]) {
@@ -635,6 +654,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
     for (int it = 0;; ++it) {
         if (tid == 0) sidx[it] = far;
         if (it == S - 1) break;
+        PN2_FPS_STAMP(0);
         // lane q < Q tests chunk q against the wave's maximum
         float lb;
         {
@@ -650,6 +670,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
 #ifdef PN2_FPS_FLOOR
         if (it > 0) act = 0u;
 #endif
+        PN2_FPS_STAMP(1);
 #ifdef PN2_FPS_STATS
         if (lane == 0) {
             atomicAdd(&g_fps_stats[0], (unsigned long long)__builtin_popcount(act));
@@ -682,6 +703,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
             }
             wave_best();
         }
+        PN2_FPS_STAMP(2);
         if constexpr (LDSC) {
             if (lane == 0) atomicMax(&key[it % 3], ((unsigned long long)wv << 32) | (0xFFFFFFFFu - wi));
             if (tid == 64) key[(it + 1) % 3] = 0ull;
@@ -701,6 +723,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
             }
             if (tid == 64) key[(it + 1) % 3] = 0ull;
             __syncthreads();
+            PN2_FPS_STAMP(3);
             const unsigned kw = (unsigned)key[it % 3];
             float4 sv = {0.f, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)};
             if (lane < NW) sv = reinterpret_cast<const float4 *>(slots)[par * NW + lane];
