@@ -99,6 +99,32 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
         const int n = tid * PPT + j;
         return (j < PPT && n < N && k < C) ? base[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
     };
+    // the packed copy first, point n on thread n % NT: each store instruction writes one
+    // contiguous run of records (a 16-byte record per lane for xyz), where the owned-points
+    // order below would scatter 4-byte stores 16*PPT bytes apart over a line per lane -- partial
+    // lines the L2 writes back, and re-reads, several times over.  The register loads after it
+    // hit the lines this pass brought into the L2.
+    if (pts_packed) {
+        for (int n = tid; n < N; n += NT) {
+            float pj[CM], sq[CM];
+#pragma unroll
+            for (int k = 0; k < CM; ++k) {
+                pj[k] = k < C ? P[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
+                sq[k] = __fmul_rn(pj[k], pj[k]);
+            }
+            const float s = layout_sum<CM>(sq, C, point_rule(kind, n, N));
+            float *dst = pts_packed + ((int64_t)b * N + n) * cp;
+            if (CM == 3 && cp == 4) {
+                *reinterpret_cast<float4 *>(dst) = make_float4(pj[0], pj[1], pj[2], s);
+            } else {
+#pragma unroll
+                for (int k = 0; k < CM; ++k)
+                    if (k < C) dst[k] = pj[k];
+                dst[C] = s;
+                for (int k = C + 1; k < cp; ++k) dst[k] = 0.f;
+            }
+        }
+    }
     int rule[PH];  // a pair shares its rule: the strided tail starts at an even index
 #pragma unroll
     for (int j = 0; j < 2 * PH; ++j) {
@@ -112,22 +138,9 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
         }
         if (j < PPT) dist[j] = valid ? __float_as_uint(1e10f) : 0u;
         if ((j & 1) == 0) rule[j >> 1] = point_rule(kind, n, N);
-        if (valid) {
-            if constexpr (LDSC) {
+        if (LDSC && valid) {
 #pragma unroll
-                for (int k = 0; k < CS; ++k) cloud[n * CS + k] = k < CM ? pj[k] : 0.f;
-            }
-            if (pts_packed) {
-                float sq[CM];
-#pragma unroll
-                for (int k = 0; k < CM; ++k) sq[k] = __fmul_rn(pj[k], pj[k]);
-                float *dst = pts_packed + ((int64_t)b * N + n) * cp;
-#pragma unroll
-                for (int k = 0; k < CM; ++k)
-                    if (k < C) dst[k] = pj[k];
-                dst[C] = layout_sum<CM>(sq, C, point_rule(kind, n, N));
-                for (int k = C + 1; k < cp; ++k) dst[k] = 0.f;
-            }
+            for (int k = 0; k < CS; ++k) cloud[n * CS + k] = k < CM ? pj[k] : 0.f;
         }
     }
     if (LDSC && tid < 3) key[tid] = 0ull;
@@ -379,6 +392,9 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b = blockIdx.x;
     const float *P = pts + (int64_t)b * sb;
+    // a cloud's element offsets fit 32 bits (the host checks): 32-bit address math keeps the
+    // prologue's per-point loads out of scratch
+    const int isn = (int)sn, isc = (int)sc;
     const int G3 = 1 << (3 * cbits);
 
     // LDS: sidx [S] | key words (8) | slots [2][NW][8] (!LDSC) | cloud [N][4] (LDSC) |
@@ -393,34 +409,25 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
     int *perm = cnt + G3;
     float *red = reinterpret_cast<float *>(perm + NT * PPT);
 
-    // ---- pass A: the points in index order (coalesced), packed records, LDS cloud copy, bbox
+    // ---- pass A: the points in index order, point n on thread n % NT (coalesced loads, one
+    // 16-byte packed record per lane per store), packed records, LDS cloud copy, bbox
     for (int e = tid; e < G3; e += NT) cnt[e] = 0;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int n = tid * PPT + j;
-        const bool valid = n < N;
+    for (int n = tid; n < N; n += NT) {
         float pa[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            pa[k] = valid ? P[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
-            if (valid) {
-                lo[k] = fminf(lo[k], pa[k]);
-                hi[k] = fmaxf(hi[k], pa[k]);
-            }
+            pa[k] = P[n * isn + k * isc];
+            lo[k] = fminf(lo[k], pa[k]);
+            hi[k] = fmaxf(hi[k], pa[k]);
         }
-        if (valid) {
-            if constexpr (LDSC) {
-                float4 r4 = {pa[0], pa[1], pa[2], 0.f};
-                reinterpret_cast<float4 *>(cloud)[n] = r4;
-            }
-            if (pts_packed) {
-                // C = 3: every layout rule sums ((x^2 + y^2) + z^2)
-                float4 r4 = {pa[0], pa[1], pa[2],
-                             __fadd_rn(__fadd_rn(__fmul_rn(pa[0], pa[0]), __fmul_rn(pa[1], pa[1])),
-                                       __fmul_rn(pa[2], pa[2]))};
-                *reinterpret_cast<float4 *>(pts_packed + ((int64_t)b * N + n) * 4) = r4;
-            }
+        if constexpr (LDSC) reinterpret_cast<float4 *>(cloud)[n] = float4{pa[0], pa[1], pa[2], 0.f};
+        if (pts_packed) {
+            // C = 3: every layout rule sums ((x^2 + y^2) + z^2)
+            const float4 r4 = {pa[0], pa[1], pa[2],
+                               __fadd_rn(__fadd_rn(__fmul_rn(pa[0], pa[0]), __fmul_rn(pa[1], pa[1])),
+                                         __fmul_rn(pa[2], pa[2]))};
+            *reinterpret_cast<float4 *>(pts_packed + ((int64_t)b * N + n) * 4) = r4;
         }
     }
 #pragma unroll
@@ -463,7 +470,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
         unsigned code = 0;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const float x = n < N ? (LDSC ? cloud[4 * n + k] : P[(int64_t)n * sn + (int64_t)k * sc]) : 0.f;
+            const float x = n < N ? (LDSC ? cloud[4 * n + k] : P[n * isn + k * isc]) : 0.f;
             const float v = (x - lo[k]) * scl[k];
             unsigned ci = (v >= 0.f && v < (float)g) ? (unsigned)v : (v >= (float)g ? (unsigned)(g - 1) : 0u);  // NaN -> 0
             // spread the (<= 4) bits of ci to every third bit
@@ -527,7 +534,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 float v = 0.f;
-                if (n >= 0) v = LDSC ? cloud[4 * n + k] : P[(int64_t)n * sn + (int64_t)k * sc];
+                if (n >= 0) v = LDSC ? cloud[4 * n + k] : P[n * isn + k * isc];
                 X[k][j] = v;
             }
         }
@@ -647,7 +654,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
     int far = (int)start[b];
     float c[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) c[k] = P[(int64_t)far * sn + (int64_t)k * sc];
+    for (int k = 0; k < 3; ++k) c[k] = P[far * isn + k * isc];
     if (tid < 3) key[tid] = 0ull;
     __syncthreads();
 
@@ -743,7 +750,7 @@ __global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ 
         if (out_pts || out_packed) {
             float q3[3];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) q3[k] = P[(int64_t)n * sn + (int64_t)k * sc];
+            for (int k = 0; k < 3; ++k) q3[k] = P[n * isn + k * isc];
             if (out_pts) {
                 float *o = out_pts + ((int64_t)b * S + i) * 3;
 #pragma unroll
@@ -1033,6 +1040,7 @@ static int dispatch_fps_cull(const float *pts, int64_t B, int64_t N, int64_t sb,
     PN2_CULL_TRY(256, 1, 2) PN2_CULL_TRY(256, 1, 4) PN2_CULL_TRY(256, 2, 2) PN2_CULL_TRY(512, 1, 2)
     PN2_CULL_TRY(1024, 1, 2) PN2_CULL_TRY(1024, 2, 2) PN2_CULL_TRY(1024, 1, 4) PN2_CULL_TRY(1024, 2, 4)
     PN2_CULL_TRY(1024, 4, 2) PN2_CULL_TRY(1024, 4, 4) PN2_CULL_TRY(1024, 8, 2)
+    PN2_CULL_TRY(256, 8, 4) PN2_CULL_TRY(512, 8, 4) PN2_CULL_TRY(512, 16, 2) PN2_CULL_TRY(512, 4, 8)
 #undef PN2_CULL_TRY
     if (N <= 512) return launch_fps_cull<256, 1, 2>(A);
     if (N <= 1024) return launch_fps_cull<256, 2, 2>(A);
@@ -1098,7 +1106,9 @@ extern "C" int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C,
         if (C == 10) return launch_fps_stream<10, true>(A, ws, st);
         return launch_fps_stream<kMaxC, false>(A, ws, st);
     }
-    if (C == 3 && N > 256 && tuning().fps_cull != 0 && tuning().fps_threads == 0)
+    // (the culled kernel addresses a cloud with 32-bit element offsets)
+    const bool off32 = sn >= 0 && sc >= 0 && (N - 1) * sn + 2 * sc < (int64_t)INT32_MAX;
+    if (C == 3 && N > 256 && off32 && tuning().fps_cull != 0 && tuning().fps_threads == 0)
         return dispatch_fps_cull(pts, B, N, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed, st);
     if (C == 3) return dispatch_fps<3, true, 16384>(A, st);
     if (C == 10) return dispatch_fps<10, true, 8192>(A, st);

@@ -21,7 +21,8 @@ DEV = "cuda"
 # (fps_cull shape NT*100 + Q*10 + PPC, N)
 SHAPES = [(25612, 512), (25612, 300), (25614, 1024), (25622, 1000), (51212, 1024), (102412, 2048),
           (102422, 4096), (102414, 3000), (102424, 8192), (102442, 8192), (102444, 16384),
-          (102444, 9000), (102482, 16384)]
+          (102444, 9000), (102482, 16384), (25684, 8192), (25684, 5000), (51284, 16384),
+          (51362, 16384), (51362, 12000), (51248, 16384)]
 
 
 def _cloud(kind, B, N, seed):

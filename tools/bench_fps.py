@@ -29,6 +29,15 @@ VARIANTS = ["64x4", "64x8", "64x16", "128x4", "128x8", "256x2", "256x4", "512x2"
             "1024x2", "1024x4", "1024x8", "1024x16", ""]
 
 
+def _cull_points(f):
+    """points per block of a forced culled shape NT*100 + Q*10 + PPC (Q may exceed 9)"""
+    for nt in (1024, 512, 256):
+        r = f - nt * 100
+        if 0 <= r < 1000:
+            return nt * (r // 10) * (r % 10)
+    return 0
+
+
 def main():
     from pn2 import tuning
     dev = torch.device("cuda")
@@ -50,7 +59,7 @@ def main():
             nt, ppt = map(int, v.split("x")) if v else (0, 0)
             if v and (nt * ppt < N or (nt * ppt >= 4 * N and not only)):
                 continue
-            if cull > 1 and (cull // 100) * ((cull // 10) % 10) * (cull % 10) < N:
+            if cull > 1 and _cull_points(cull) < N:
                 continue
             if v == "" and cull != 1:
                 v = "cull=%d" % cull
