@@ -705,8 +705,8 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
                 if (ue < 0) break;  // units are used in order: the rest of the slab is unused
                 float mx = fmaxf(fmaxf(acc[4 * k], acc[4 * k + 1]), fmaxf(acc[4 * k + 2], acc[4 * k + 3]));
                 float mn = fminf(fminf(acc[4 * k], acc[4 * k + 1]), fminf(acc[4 * k + 2], acc[4 * k + 3]));
-                mx = fmaxf(mx, swap_halves(mx));
-                mn = fminf(mn, swap_halves(mn));
+                mx = max_halves(mx);
+                mn = min_halves(mn);
                 if ((ue >> 8) != sg) {
                     flush();
                     sg = ue >> 8;
@@ -724,8 +724,8 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
             for (int k = 0; k < 4; ++k) {  // rows 8k..8k+7 of the slab: registers 4k..4k+3, both halves
                 mx[k] = fmaxf(fmaxf(acc[4 * k], acc[4 * k + 1]), fmaxf(acc[4 * k + 2], acc[4 * k + 3]));
                 mn[k] = fminf(fminf(acc[4 * k], acc[4 * k + 1]), fminf(acc[4 * k + 2], acc[4 * k + 3]));
-                mx[k] = fmaxf(mx[k], swap_halves(mx[k]));
-                mn[k] = fminf(mn[k], swap_halves(mn[k]));
+                mx[k] = max_halves(mx[k]);
+                mn[k] = min_halves(mn[k]);
             }
             if (h == 0) {
                 if (A.K == 8) {
@@ -751,7 +751,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
                 mx = fmaxf(mx, acc[q]);
                 mn = fminf(mn, acc[q]);
             }
-            const float m = fin(fmaxf(mx, swap_halves(mx)), fminf(mn, swap_halves(mn)));
+            const float m = fin(max_halves(mx), min_halves(mn));
             const unsigned gg = ((unsigned)slab * 32u) / (unsigned)A.K;
             if (h == 0 && (unsigned)slab * 32u < (unsigned)A.M) {
                 if (A.pool_mode == 0) A.out[(int64_t)gg * A.ostride + col] = m;

@@ -352,8 +352,8 @@ void dense_split_kernel(const DenseSplitArgs A) {
             for (int k = 0; k < 4; ++k) {
                 mx[k] = fmaxf(fmaxf(acc[i][4 * k], acc[i][4 * k + 1]), fmaxf(acc[i][4 * k + 2], acc[i][4 * k + 3]));
                 mn[k] = fminf(fminf(acc[i][4 * k], acc[i][4 * k + 1]), fminf(acc[i][4 * k + 2], acc[i][4 * k + 3]));
-                mx[k] = fmaxf(mx[k], swap_halves(mx[k]));
-                mn[k] = fminf(mn[k], swap_halves(mn[k]));
+                mx[k] = max_halves(mx[k]);
+                mn[k] = min_halves(mn[k]);
             }
             if (h == 0) {
                 const int per = A.K / 8;  // register groups per output group
@@ -389,7 +389,7 @@ void dense_split_kernel(const DenseSplitArgs A) {
             mx = fmaxf(mx, acc[i][q]);
             mn = fminf(mn, acc[i][q]);
         }
-        const float m = fin(fmaxf(mx, swap_halves(mx)), fminf(mn, swap_halves(mn)));
+        const float m = fin(max_halves(mx), min_halves(mn));
         // ReLU output >= +0: its bits order as uints; signed (norelu) values go through fkey
         const unsigned mk = A.norelu ? fkey(m) : __float_as_uint(m);
         if (h == 0 && slab_row < A.M) {
@@ -727,8 +727,8 @@ void dense_lds_kernel(const DenseSplitArgs A) {
             mx = fmaxf(mx, acc[i][q]);
             mn = fminf(mn, acc[i][q]);
         }
-        mx = fmaxf(mx, swap_halves(mx));
-        mn = fminf(mn, swap_halves(mn));
+        mx = max_halves(mx);
+        mn = min_halves(mn);
         const float y = __builtin_fmaf(al >= 0.f ? mx : mn, al, be);
         const float m = A.norelu ? y : chain_relu(y);
         // ReLU output >= +0: its bits order as uints; signed (norelu) values go through fkey

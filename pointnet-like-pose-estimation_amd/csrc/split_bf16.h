@@ -109,9 +109,16 @@ __device__ __forceinline__ Split ring_readN(const char *slot, int lane) {
     }
 }
 
-// lanes l and l^32 exchange x (the two halves of a 32x32 tile column)
-__device__ __forceinline__ float swap_halves(float x) {
-    return __shfl_xor(x, 32);
+// max / min of x over lanes l and l^32 (the two halves of a 32x32 tile column): one
+// v_permlane32_swap (a VALU lane exchange) in place of a ds_bpermute LDS round trip.  The swap
+// leaves lane l < 32 with (x[l], x[l+32]) and lane l >= 32 with (x[l-32], x[l]).
+__device__ __forceinline__ float max_halves(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float min_halves(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fminf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
