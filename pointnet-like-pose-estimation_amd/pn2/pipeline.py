@@ -236,6 +236,9 @@ class PipelinedForward:
                 starts[id(sa)] = shard.device_start(B, n, dev)
                 n = sa.point_number
         entries = {}
+        # geometry_bq = 0: the ball queries run in each batch's forward instead (the module
+        # queries when its entry holds no lists), leaving the FPS alone on the geometry stream
+        bq = bool(tuning.get("geometry_bq"))
         pts = x.permute(0, 2, 1)
         first = {}  # chain -> (newp, cpk, ppk) of its first layer
         heads = [ch[0] for ch in chains]
@@ -261,7 +264,7 @@ class PipelinedForward:
                     rk = list(zip(sa.radius_list, sa.sample_number_list))
                 else:
                     rk = [(sa.radius, sa.sample_number)]
-                idxs = [ops.ball_query_direct(ppk, cpk, C, r, kk, True) for r, kk in rk]
+                idxs = [ops.ball_query_direct(ppk, cpk, C, r, kk, True) for r, kk in rk] if bq else []
                 entries[id(sa)] = (p.data_ptr(), newp, cpk, ppk, idxs)
                 p = newp
         return entries

@@ -22,6 +22,8 @@ Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_s
                      hardware queues: GPU_MAX_HW_QUEUES >= the pipeline's streams)
     force_gather     1: shard.all_gather_rows runs its collective in a 1-rank group too (the
                      bench's --force-rccl measurement of the collective's cost on one GPU)
+    geometry_bq      1: the pipeline's geometry stream runs the ball queries after the FPS;
+                     0: only the FPS, each batch's forward (compute stream) queries
 
 Unknown keys are an error.  ``override(**kw)`` changes keys for the duration of a ``with``
 block (tests).  Every default is the measured best.
@@ -39,6 +41,7 @@ HOST_DEFAULTS = {
     "fc_tail": 1,
     "force_gather": 0,
     "tail_streams": 1,
+    "geometry_bq": 1,
 }
 
 
