@@ -48,6 +48,18 @@ __device__ __forceinline__ unsigned row_max_u32(unsigned v) {
 // register file with every channel keep only xyz (CR = 3) or nothing (CR = 0) there and re-read
 // the other channels of their points from the input each iteration (slow, but any N up to
 // NT*PPT); a cloud whose extra channels are constant (the one-hot class) never reads them.
+#ifdef PN2_FPS_WGSTAMPS
+// Diagnostic builds only (tools/debug/fps_wg.py): s_memrealtime (100 MHz) at entry and exit of
+// every fps_kernel workgroup, in dispatch-counter order (65536 slots, wrapping)
+__device__ unsigned g_fps_wgctr;
+__device__ unsigned long long g_fps_wg[65536 * 2];
+extern "C" int pn2_debug_fps_wg(unsigned long long *out, unsigned *count) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(count, HIP_SYMBOL(g_fps_wgctr), sizeof(unsigned)) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fps_wg), sizeof(g_fps_wg)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 template <int NT, int PPT, int CM, bool FIXED, bool LDSC, int CR = CM>
 __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, int N, int Crt,
                                                  int64_t sb, int64_t sn, int64_t sc, int kind,
@@ -62,6 +74,13 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
     // dependent chain (one short VALU burst, a reduction and a barrier per iteration) is the
     // pipeline's critical path: its waves take issue priority over co-resident waves.
     __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
+#ifdef PN2_FPS_WGSTAMPS
+    unsigned wg_slot = 0;
+    if (threadIdx.x == 0) {
+        wg_slot = atomicAdd(&g_fps_wgctr, 1u) & 65535u;
+        g_fps_wg[2 * wg_slot] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     constexpr int SLOT = (CM + 2 + 3) & ~3;  // {max, index, coords...} padded to 16 bytes
     const int C = FIXED ? CM : Crt;
     const int tid = threadIdx.x;
@@ -324,6 +343,9 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
             }
         }
     }
+#ifdef PN2_FPS_WGSTAMPS
+    if (threadIdx.x == 0) g_fps_wg[2 * wg_slot + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // ------------------------------------------------------------------------- culled FPS (C = 3)

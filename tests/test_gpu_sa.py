@@ -471,3 +471,33 @@ def test_eval_with_autograd_is_differentiable():
     assert not fz[0].requires_grad
     for a, b in zip(fz, want):
         np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
+@pytest.mark.parametrize("head", ["ClsSSG", "ClsMSG"])
+def test_graphed_pipeline_ball_query_in_forward_matches_eager(head):
+    """tuning geometry_bq = 0: the geometry graph holds only the FPS launches and each batch's sa
+    graph runs its layers' ball queries itself (the module queries when its provided entry holds
+    no lists).  Results and generator state are still the eager ones, bit for bit."""
+    from pn2 import heads as H
+    from pn2 import tuning
+    from pn2.pipeline import GraphedPipeline
+    torch.manual_seed(8)
+    model = getattr(H, head)().eval()
+    cases.randomize_bn(model, 8)
+    model = model.to(DEV)
+    B, N = (8, 2048) if head == "ClsMSG" else (16, 1024)
+    xs = [cases.cloud("uniform3", B, N, 300 + i).permute(0, 2, 1).contiguous().to(DEV) for i in range(5)]
+    torch.manual_seed(23)
+    with torch.no_grad():
+        want = [[t.cpu().numpy() for t in model(x)] for x in xs]
+    rng_want = torch.randint(0, 1 << 30, (4,))
+    with tuning.override(geometry_bq=0):
+        gp = GraphedPipeline(model)
+        torch.manual_seed(23)
+        got = [[t.cpu().numpy() for t in o] for o in gp.run(xs)]
+        for ent in gp._slots[0].entries.values():
+            assert ent[4] == []  # no ball query in the geometry graph
+    np.testing.assert_array_equal(torch.randint(0, 1 << 30, (4,)).numpy(), rng_want.numpy())
+    for i, (g, w) in enumerate(zip(got, want)):
+        for k, (a, b) in enumerate(zip(g, w)):
+            np.testing.assert_array_equal(a, b, err_msg="output %d of batch %d" % (k, i))
