@@ -476,14 +476,10 @@ class GraphedPipeline(PipelinedForward):
         self.ngroups = self.nslots // gb
         self.geometry_streams = int(geometry_streams)
         self.trace = None
-        self._key = None
+        self._key = None  # (input signature, precision) the slots were captured for
+        self._params = None  # graphs.ParamState of the model
+        self._pkey = None  # its key at the last capture
         self._slots = None  # the group slots
-
-    def _state_key(self, x, extra):
-        from .graphs import _module_tensors, _sig
-        ts = _module_tensors(self.model)
-        return (_sig((x,) + tuple(extra)), ops.current_precision()) + tuple(
-            (t.data_ptr(), t._version) for t in ts)
 
     def _split_index(self):
         """The SA module after which a slot's compute graph ends and its tail graph begins.  The
@@ -540,28 +536,40 @@ class GraphedPipeline(PipelinedForward):
             entries = self._fps_chain(grp.x)
             grp.fps.capture_end()
         torch.cuda.synchronize(dev)
-        # each batch's slice of the group's geometry, keyed by the tensor its SA module is
-        # called with in that batch's forward (its slice of the input or of the previous
-        # layer's centroids)
+        grp.entries = entries
+        grp.B = B
+        grp.halves = [self._capture_forward(xs[h], extra, dev, *self._half_entries(grp, h))
+                      for h in range(gb)]
+        return grp
+
+    def _half_entries(self, grp, h):
+        """Batch h's slice of the group's geometry, keyed by the tensor its SA module is called
+        with in that batch's forward (its slice of the input or of the previous layer's
+        centroids), and the storages of the group's geometry outputs."""
+        B = grp.B
         srcs = {grp.x.data_ptr(): grp.x}
-        for _, newp, _, _, _ in entries.values():
+        for _, newp, _, _, _ in grp.entries.values():
             srcs[newp.data_ptr()] = newp
 
-        def part(t, h):
+        def part(t):
             return t[h * B:(h + 1) * B]
 
         geo = set()
-        for _, newp, cpk, ppk, idxs in entries.values():
+        for _, newp, cpk, ppk, idxs in grp.entries.values():
             geo.update(t.untyped_storage().data_ptr()
                        for t in [newp, cpk, ppk] + [t for ic in idxs for t in ic])
-        grp.halves = []
-        for h in range(gb):
-            ent = {k: (part(srcs[ptr], h).data_ptr(), part(newp, h), part(cpk, h), part(ppk, h),
-                       [tuple(part(t, h) for t in ic) for ic in idxs])
-                   for k, (ptr, newp, cpk, ppk, idxs) in entries.items()}
-            grp.halves.append(self._capture_forward(xs[h], extra, dev, ent, geo))
-        grp.entries = entries
-        return grp
+        ent = {k: (part(srcs[ptr]).data_ptr(), part(newp), part(cpk), part(ppk),
+                   [tuple(part(t) for t in ic) for ic in idxs])
+               for k, (ptr, newp, cpk, ppk, idxs) in grp.entries.items()}
+        return ent, geo
+
+    def _recapture_forwards(self, extra, dev):
+        """New sa / head graphs for every batch slot after a parameter change (their kernels
+        read the parameters' memory); the geometry graphs read only coordinates and draws, and
+        are kept."""
+        for grp in self._slots:
+            grp.halves = [self._capture_forward(sl.x, extra, dev, *self._half_entries(grp, h))
+                          for h, sl in enumerate(grp.halves)]
 
     def _capture_forward(self, x, extra, dev, entries, geo):
         sl = _Slot()
@@ -604,21 +612,27 @@ class GraphedPipeline(PipelinedForward):
         if not batches:
             return []
         extra_of = (lambda i: ()) if extras is None else (lambda i: tuple(extras[i]))
-        key = self._state_key(batches[0], extra_of(0))
-        # the other batches need only the same input signature (the full key walks every
-        # parameter and buffer: ~30 us of host time per batch before the first launch, all of it
-        # GPU idle time inside a timed run); a batch list repeating one input needs nothing
-        from .graphs import _sig
+        from .graphs import ParamState, _sig
         x0, e0 = batches[0], extra_of(0)
+        sig = (_sig((x0,) + tuple(e0)), ops.current_precision())
+        # the other batches need only the same input signature; a batch list repeating one
+        # input needs nothing
         for i in range(1, len(batches)):
             x = batches[i]
             if x is x0 and (extras is None or all(a is b for a, b in zip(extra_of(i), e0))):
                 continue
-            if _sig((x,) + extra_of(i)) != key[0]:
+            if _sig((x,) + extra_of(i)) != sig[0]:
                 return self._run_eager(batches, extras, post, False)  # mixed shapes: eager
+        if self._params is None:
+            self._params = ParamState(self.model)
         outs, first = [], 0
         dev = batches[0].device
-        if key != self._key or self._slots is None:
+        # With the same input signature the parameters (the sa / head graphs read their memory)
+        # are checked only after the first geometry group is issued: the geometry graphs read
+        # coordinates and draws alone, and the check's host time (a walk over every parameter
+        # and buffer, ~40-110 us) then overlaps that group's FPS instead of delaying it.
+        check_params = self._slots is not None and sig == self._key
+        if not check_params:
             self._slots = None
             draws = []
 
@@ -632,7 +646,8 @@ class GraphedPipeline(PipelinedForward):
             self._draws = draws
             self._slots = [self._capture(batches[0], extra_of(0), dev, draws)
                            for _ in range(self.ngroups)]
-            self._key = self._state_key(batches[0], extra_of(0))
+            self._key = sig
+            self._pkey = self._params.key()  # capture allocations do not touch parameters
             # replay every captured graph once now, in dependency order on this stream (start
             # index 0: a valid point; outputs land in static buffers that real replays
             # overwrite; no RNG inside the graphs): a graph's first launch costs extra, and
@@ -656,8 +671,9 @@ class GraphedPipeline(PipelinedForward):
         mains = [main] + ([_extra_compute_stream(dev.index)] if self.compute_streams == 2 else [])
         tails = [tail] + ([_extra[dev.index][2]] if self.tail_streams == 2 else [])
         caller = torch.cuda.current_stream(dev)
+        ev0 = caller.record_event()  # one event for every pipeline stream to wait on
         for st in geos + mains + tails:
-            st.wait_stream(caller)
+            st.wait_event(ev0)
         # per group slot: the fps replay's event, and the events after which the group's
         # batches no longer read its inputs / geometry (one per batch: with two compute
         # streams they finish on different streams)
@@ -719,8 +735,14 @@ class GraphedPipeline(PipelinedForward):
                 g, h = divmod(i - first, gb)
                 s = g % ng
                 bs = s * gb + h
-                sl = self._slots[s].halves[h]
                 top_up(g, -1)
+                if check_params:  # (first batch: its group's geometry is issued)
+                    check_params = False
+                    pk = self._params.key()
+                    if pk != self._pkey:
+                        self._recapture_forwards(extra_of(i), dev)
+                        self._pkey = self._params.key()
+                sl = self._slots[s].halves[h]
                 main = mains[(i - first) % len(mains)]
                 with torch.cuda.stream(main):
                     main.wait_event(ev_fps[s])
@@ -807,7 +829,7 @@ class GraphedPipeline(PipelinedForward):
             for B, N in self._draws:
                 dst = buf[g, off + h * B:off + (h + 1) * B]
                 if h < nh:
-                    dst.copy_(shard.draw_start(B, N, pin=False))
+                    shard.draw_start_into(dst, N)
                 else:
                     dst.zero_()
                 off += gb * B

@@ -49,6 +49,18 @@ def draw_start(B, N, pin=True):
     return t.pin_memory() if pin and torch.cuda.is_available() else t
 
 
+def draw_start_into(dst, N):
+    """draw_start(len(dst), N) written into the CPU int64 vector dst: the same draw (the same
+    generator consumption and values), straight into dst when this process draws the whole
+    batch -- the pipeline's pinned start rows, without a temporary and a copy per draw."""
+    spec = getattr(_state, "spec", None)
+    B = dst.shape[0]
+    if spec is None or (spec[0] == B and spec[1] == 0):
+        torch.randint(0, N, (B,), dtype=torch.long, out=dst)
+    else:
+        dst.copy_(draw_start(B, N, pin=False))
+
+
 def device_start(B, N, device):
     """The FPS start draw as a device tensor.  Inside a graph capture (graphs.GraphedForward)
     the draw is not taken here: the capture reads a static device slot that every replay

@@ -193,6 +193,8 @@ def test_config_full_batch_pipeline_equals_eager(cfg, monkeypatch):
         return t.clone()
 
     monkeypatch.setattr(shard, "draw_start", fixed_draw)
+    # the pipeline writes its draws in place (shard.draw_start_into): the same cycle
+    monkeypatch.setattr(shard, "draw_start_into", lambda dst, N: dst.copy_(fixed_draw(dst.shape[0], N)))
     xd, md = x.to(DEV), mean.to(DEV)
     eager = _forward(names, models, xd, md, prec)
     model = models[0] if len(models) == 1 else MultiHead(

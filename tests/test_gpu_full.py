@@ -116,6 +116,8 @@ def test_full_size_head_graphed_pipeline_matches_reference(name, monkeypatch):
         return d.clone()
 
     monkeypatch.setattr(shard, "draw_start", golden_draw)
+    # the pipeline writes its draws in place (shard.draw_start_into): the same cycle
+    monkeypatch.setattr(shard, "draw_start_into", lambda dst, N: dst.copy_(golden_draw(dst.shape[0], N)))
     acts, tags, hs = _hook_acts(model)  # fire on the eager first batch only (graphs replay)
     n = 4
     extras = [tuple(args[1:])] * n if len(args) > 1 else None

@@ -355,8 +355,11 @@ def test_graphed_pipeline_matches_eager(head, tail):
     with torch.no_grad():
         want2 = [as_np(model(x, *(extras[i] if extras else ()))) for i, x in enumerate(xs[:3])]
     torch.manual_seed(5)
+    old_sa = [sl.sa for grp in gp._slots for sl in grp.halves]
     got2 = [as_np(o) for o in gp.run(xs[:3], extras[:3] if extras else None)]
-    assert gp._slots is not slots
+    # the sa / head graphs were recaptured (the geometry graphs read no parameters and stay)
+    new_sa = [sl.sa for grp in gp._slots for sl in grp.halves]
+    assert all(a is not b for a, b in zip(new_sa, old_sa))
     for g, w in zip(got2, want2):
         for a, b in zip(g, w):
             np.testing.assert_array_equal(a, b)
