@@ -1,0 +1,52 @@
+"""Is the pipelined SSG run host-bound?  For K batches: the host time run() takes to issue
+everything (it returns before the GPU is done) against the whole run's time (to the final
+synchronize), and the same with the bench's `post` (the per-batch logits gather).
+    python tools/debug/host_bound.py"""
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "pointnet-like-pose-estimation_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+import cases  # noqa: E402
+from pn2 import heads as H  # noqa: E402
+from pn2 import shard  # noqa: E402
+from pn2.pipeline import GraphedPipeline  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def main():
+    torch.manual_seed(8)
+    model = H.ClsSSG().eval()
+    cases.randomize_bn(model, 8)
+    model = model.to(DEV)
+    x = cases.cloud("uniform3", 32, 1024, 90).permute(0, 2, 1).contiguous().to(DEV)
+    gp = GraphedPipeline(model)
+
+    def post(i, o):
+        return shard.all_gather_rows(o[0], sizes="shard")
+
+    with torch.no_grad():
+        gp.run([x] * 12)
+    torch.cuda.synchronize()
+    for K in (20, 100):
+        for name, p in (("no post", None), ("gather post", post)):
+            for _ in range(2):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                with torch.no_grad(), shard.batch_shard(32, 0):
+                    gp.run([x] * K, post=p)
+                t1 = time.perf_counter()
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                print("K=%3d %-11s host issue %7.0f us (%5.1f us/batch), whole run %7.0f us (%5.1f us/batch), %.0f clouds/s" % (
+                    K, name, (t1 - t0) * 1e6, (t1 - t0) * 1e6 / K, (t2 - t0) * 1e6, (t2 - t0) * 1e6 / K,
+                    32 * K / (t2 - t0)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,9 @@
+# r04: the pipeline's sensitivity to the chains (timing-only ablation builds of sa_chain.hip)
+export TMPDIR=/tmp
+OUT=gpurun_out/r04t; mkdir -p $OUT
+V=pointnet-like-pose-estimation_amd/pn2/var
+for i in 1 2; do for v in base NODMA NOEPI ALL; do
+  env=""; [ $v != base ] && env="PN2_TUNING=lib=$V/abl_$v.so"
+  env $env timeout -k 10 300 python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-kernel-timer > $OUT/b.log 2>&1 || exit $?
+  echo "$v K100 $i $(grep '^{' $OUT/b.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["eager_value"])')"
+done; done
