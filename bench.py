@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU baseline sample")
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--no-settled", action="store_true",
+                    help="skip the second pipelined measurement after an ~80 ms settle")
     ap.add_argument("--graph", action="store_true", help="replay the forward as a HIP graph")
     ap.add_argument("--eager-pipeline", action="store_true",
                     help="pipelined launch issued op by op (pn2.pipeline.PipelinedForward) "
@@ -481,6 +483,18 @@ def main():
     ms = el / a.steps * 1e3
     value = gB * a.steps / el
     eager_value = value
+    # The same K batches again once the device has been busy for a while (untimed pipelined
+    # batches for ~80 ms first): after an idle gap the SOC clock sits in deep sleep (38-47 MHz)
+    # and needs ~30 ms of load to reach 1200 MHz, and a pipelined run at a low SOC clock is up
+    # to 25 % slower (tools/debug/clock_trace.py).  `value` above is the
+    # contract's number (W warm-up steps, then K timed); this one is reported beside it.
+    settled = None
+    if pipelined and not a.no_settled:
+        run_pipelined(max(a.steps, int(80.0 / max(ms, 1e-3)) + 1))
+        el_s, _ = timed(a.steps, False, pipe=True)
+        el_s = max_over_ranks(el_s)
+        settled = {"value": round(gB * a.steps / el_s, 2), "ms_per_step": round(el_s / a.steps * 1e3, 4),
+                   "settle": "~80 ms of untimed pipelined batches before the same K timed steps"}
     if a.graph or pipelined:
         el_e, _ = timed(a.steps, False, eager_models)
         eager_value = gB * a.steps / max_over_ranks(el_e)
@@ -567,6 +581,7 @@ def main():
                            if not a.eager_pipeline else "")
                        if pipelined else "eager"),
             "eager_value": round(eager_value, 2),
+            "value_settled": settled,
             # hardware queues of this process (bench.py sets 8 unless --hw-queues 0; HIP's own
             # default is 4: DESIGN.md §6)
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default (4)"),

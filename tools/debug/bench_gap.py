@@ -5,7 +5,14 @@ it).  python tools/debug/bench_gap.py VARIANT
   benchin  bench.py's model and input (build_models / make_inputs), otherwise bare
   eagerw   benchin + bench's 10 eager warm-up steps before the pipeline
   batched  eagerw + bench's BatchedGather(8) post
-  prec     batched + pn2.mlp_precision('fp32') entered for the whole run, as bench does"""
+  prec     batched + pn2.mlp_precision('fp32') entered for the whole run, as bench does
+  warmk    bare with a 100-batch pipelined warm-up
+  empty    bare, torch.cuda.empty_cache() before every timed run
+  sleep    bare, 200 ms idle before every timed run
+  spin     bare, 200 ms host busy-wait (GPU idle) before every timed run
+  gpubusy  bare, 200 ms of GPU matmuls (host asleep) before every timed run
+(The first timed run after a short warm-up reads ~5 % below the later ones in every variant
+above; these three ask why.)"""
 import os
 import sys
 import time
@@ -27,7 +34,7 @@ DEV = torch.device("cuda", 0)
 def main():
     v = sys.argv[1]
     order = ["bare", "benchin", "eagerw", "batched", "prec"]
-    lvl = order.index(v)
+    lvl = order.index(v) if v in order else 0
     if lvl >= 4:
         pn2.mlp_precision("fp32").__enter__()
     if lvl >= 1:
@@ -52,11 +59,34 @@ def main():
             return lambda i, o: bg(i, o[0])
         return lambda i, o: shard.all_gather_rows(o[0], sizes="shard")
 
+    nw = 100 if v == "warmk" else 10
     with shard.batch_shard(32, 0):
-        gp.run([x] * 10, post=post_for(10))
+        gp.run([x] * nw, post=post_for(nw))
     torch.cuda.synchronize()
     res = []
     for _ in range(3):
+        if v == "empty":
+            torch.cuda.empty_cache()
+        if v == "sleep":
+            time.sleep(0.2)
+        if v == "spin":
+            t1 = time.perf_counter() + 0.2
+            while time.perf_counter() < t1:
+                pass
+        if v == "gpubusy":
+            a = torch.randn(4096, 4096, device="cuda")
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(20):
+                a = a @ a
+                a = a / a.norm()
+            torch.cuda.synchronize()
+            n = max(1, int(0.2 / max(time.perf_counter() - t1, 1e-4) * 20))
+            for _ in range(n):
+                a = a @ a
+                a = a / a.norm()
+            time.sleep(0.15)
+            torch.cuda.synchronize()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         with shard.batch_shard(32, 0):
