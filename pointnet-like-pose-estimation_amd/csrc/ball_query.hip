@@ -243,332 +243,9 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
     }
 }
 
-// ------------------------------------------------------------------ grid ball query (xyz)
-// For xyz clouds the scan above tests every centroid against all N points (SSG sa1: 524k pairs
-// per cloud for ~8 hits per centroid).  Here a workgroup of NT = 64*WV consecutive centroids of
-// one cloud first bins the cloud into a grid in LDS, then each lane tests only the points of
-// the cells its ball can reach:
-//   1. the cloud's records into registers; bounding box and largest ssq of the finite records
-//      (wave shuffles + LDS across waves);
-//   2. per axis G = floor(extent / r) cells (1..16, so a cell is at least one radius wide),
-//      each record's cell, and its rank within the cell from the LDS counter's atomic add;
-//      records with a non-finite value go to an overflow list every lane scans (NaN distances
-//      are hits under the reference's !(d > r^2) test, pointnet2_utils.py:85);
-//   3. exclusive scan of the cell counts (the cell starts), then the records and their
-//      indices scattered into cell order;
-//   4. per lane: the cells that intersect [c - rr, c + rr] on every axis, rr = the radius
-//      widened by a bound on the distance formula's rounding error (2^-16 (ssq_c + max ssq),
-//      ~60x the worst-case error of the three-rounding formula), so every point the reference
-//      counts as a hit lies in a scanned cell.  A row of cells along x is one contiguous range
-//      of records, read 8 at a time (the loads of a batch issue together); each candidate is
-//      tested with the same distance expression and test as the scan kernel (bq_dist), and a
-//      hit sets bit n of the lane's index-ordered bitmask in LDS (ds_or, no return);
-//   5. rows out, one centroid per wave step: the row's mask words across the lanes, a wave
-//      prefix sum of their popcounts gives each word's first output slot, so the first K hits
-//      in index order (the reference's sort + slice, pointnet2_utils.py:86-87) are stored
-//      straight into the row, coalesced, then the padding.  No row buffer: any K <= N.
-// Exact for any input (a non-finite centroid scans the whole cloud); the cell culling is only
-// effective while the radius is small against the cloud's extent (host rule in launch_bq_grid).
-constexpr int kGridAxis = 16;
-constexpr int kGridCells = kGridAxis * kGridAxis * kGridAxis;
-
-__host__ __device__ inline size_t bq_grid_align(size_t x) { return (x + 15) & ~(size_t)15; }
-
-// dynamic LDS bytes of ball_query_grid_kernel: records, indices, cell starts, masks, and the
-// row buffer (rows > 0: NT rows of K + 1 entries of osz bytes)
-__host__ __device__ inline size_t bq_grid_lds(int N, int NT, int rows, int osz) {
-    size_t o = bq_grid_align((size_t)N * 16);
-    o = bq_grid_align(o + (size_t)N * 4);
-    o = bq_grid_align(o + (size_t)(kGridCells + 1) * 4);
-    return o + (size_t)(((N + 31) >> 5) + 1) * NT * 4 + (size_t)rows * NT * osz;
-}
-
-__device__ __forceinline__ bool rec_finite(const float4 &p) {
-    return isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && isfinite(p.w);
-}
-
-template <int WV, int PPT, typename OT>
-__global__ __launch_bounds__(64 * WV) void ball_query_grid_kernel(
-    const float *__restrict__ pts, const float *__restrict__ ctr, int N, int S, float r2, int K,
-    OT *__restrict__ out, int *__restrict__ out_cnt, int rowbuf, int stop) {
-    constexpr int NT = 64 * WV;
-    constexpr int BATCH = 8;
-    extern __shared__ __attribute__((aligned(16))) char bq_dyn[];
-    const int NWD = (N + 31) >> 5;
-    const int MS = NWD + 1;  // mask row stride (words): lane-major, odd -> few bank conflicts
-    size_t o = 0;
-    float4 *spts = reinterpret_cast<float4 *>(bq_dyn);  // [N] records in cell order
-    o = bq_grid_align((size_t)N * 16);
-    int *sidx = reinterpret_cast<int *>(bq_dyn + o);  // [N] their indices
-    o = bq_grid_align(o + (size_t)N * 4);
-    int *cstart = reinterpret_cast<int *>(bq_dyn + o);  // [cells + 1] counts, then starts
-    o = bq_grid_align(o + (size_t)(kGridCells + 1) * 4);
-    unsigned *mask = reinterpret_cast<unsigned *>(bq_dyn + o);  // [NT][MS] hit bits
-    __shared__ float red[WV][7];
-    __shared__ int wsum[WV];
-    __shared__ int nbad;
-    __shared__ int nrow[NT], frow[NT];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int gpc = (S + NT - 1) / NT;
-    const int bid = (int)xcd_contiguous(blockIdx.x, gridDim.x);  // a cloud's groups on one XCD
-    const int b = bid / gpc;
-    const int g0 = (bid - b * gpc) * NT;
-    const float4 *src = reinterpret_cast<const float4 *>(pts) + (int64_t)b * N;
-
-    // 1. records, box, zeroed counters and masks
-    for (int i = tid; i <= kGridCells; i += NT) cstart[i] = 0;
-    for (int i = tid; i < MS * NT; i += NT) mask[i] = 0u;
-    if (tid == 0) nbad = 0;
-    float4 pr[PPT];
-    float v[7] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY, 0.f};
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int n = tid + j * NT;
-        if (n < N) {
-            pr[j] = src[n];
-            if (rec_finite(pr[j])) {
-                v[0] = fminf(v[0], pr[j].x); v[1] = fminf(v[1], pr[j].y); v[2] = fminf(v[2], pr[j].z);
-                v[3] = fmaxf(v[3], pr[j].x); v[4] = fmaxf(v[4], pr[j].y); v[5] = fmaxf(v[5], pr[j].z);
-                v[6] = fmaxf(v[6], pr[j].w);
-            }
-        }
-    }
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) v[k] = fminf(v[k], __shfl_xor(v[k], d));
-#pragma unroll
-        for (int k = 3; k < 7; ++k) v[k] = fmaxf(v[k], __shfl_xor(v[k], d));
-    }
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < 7; ++k) red[w][k] = v[k];
-    __syncthreads();
-#pragma unroll
-    for (int x = 0; x < WV; ++x) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) v[k] = fminf(v[k], red[x][k]);
-#pragma unroll
-        for (int k = 3; k < 7; ++k) v[k] = fmaxf(v[k], red[x][k]);
-    }
-    // 2. the grid: cells at least one radius wide, at most 16 per axis
-    const float h = sqrtf(r2) * 1.001f;
-    float lo[3], inv[3];
-    int G[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float ext = v[3 + a] - v[a];
-        lo[a] = isfinite(v[a]) ? v[a] : 0.f;
-        const float g = (ext > 0.f && isfinite(ext) && h > 0.f) ? floorf(ext / h) : 1.f;
-        G[a] = (int)fminf(fmaxf(g, 1.f), (float)kGridAxis);
-        inv[a] = (G[a] > 1) ? (float)G[a] / ext : 0.f;
-    }
-    auto cellc = [&](float x, int a) {  // monotone in x; NaN -> 0
-        return (int)fminf(fmaxf((x - lo[a]) * inv[a], 0.f), (float)(G[a] - 1));
-    };
-    int cid[PPT], rk[PPT];
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int n = tid + j * NT;
-        cid[j] = -1;
-        rk[j] = 0;
-        if (n < N) {
-            if (rec_finite(pr[j])) {
-                cid[j] = (cellc(pr[j].z, 2) * G[1] + cellc(pr[j].y, 1)) * G[0] + cellc(pr[j].x, 0);
-                rk[j] = atomicAdd(&cstart[cid[j]], 1);
-            } else {
-                rk[j] = atomicAdd(&nbad, 1);
-            }
-        }
-    }
-    __syncthreads();
-    // 3. cell starts (exclusive scan, a chunk of consecutive cells per thread), then scatter
-    const int ncell = G[0] * G[1] * G[2];
-    const int cpt = (ncell + NT - 1) / NT;
-    const int c0 = min(tid * cpt, ncell), c1 = min(c0 + cpt, ncell);
-    int mine = 0;
-    for (int i = c0; i < c1; ++i) mine += cstart[i];
-    int incl = mine;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int t = __shfl_up(incl, d);
-        if (lane >= d) incl += t;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    int run = incl - mine, nfin = 0;
-#pragma unroll
-    for (int x = 0; x < WV; ++x) {
-        if (x < w) run += wsum[x];
-        nfin += wsum[x];
-    }
-    for (int i = c0; i < c1; ++i) {
-        const int c = cstart[i];
-        cstart[i] = run;
-        run += c;
-    }
-    if (tid == 0) cstart[ncell] = nfin;
-    __syncthreads();
-    if (stop == 9) {  // debug: this workgroup's grid parameters into out_cnt
-        if (tid == 0 && out_cnt) {
-            int *d = out_cnt + (int64_t)blockIdx.x * 16;
-            d[0] = G[0]; d[1] = G[1]; d[2] = G[2]; d[3] = nfin;
-            for (int a = 0; a < 3; ++a) { d[4 + a] = __float_as_int(lo[a]); d[7 + a] = __float_as_int(inv[a]); }
-            d[10] = __float_as_int(v[6]); d[11] = __float_as_int(v[3]); d[12] = __float_as_int(h);
-            d[13] = cstart[0]; d[14] = cstart[1]; d[15] = cstart[ncell / 2];
-        }
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int n = tid + j * NT;
-        if (n < N) {
-            const int pos = (cid[j] >= 0 ? cstart[cid[j]] : nfin) + rk[j];
-            spts[pos] = pr[j];
-            sidx[pos] = n;
-        }
-    }
-    __syncthreads();
-    if (stop == 2) return;
-
-    // 4. this lane's centroid against the records of the cells its ball reaches
-    const int s = g0 + tid;
-    if (s < S) {
-        const float4 c4 = reinterpret_cast<const float4 *>(ctr)[(int64_t)b * S + s];
-        const float c[4] = {c4.x, c4.y, c4.z, c4.w};
-        unsigned *mrow = mask + tid * MS;
-        // records [j, j1) of the cell order, BATCH loads in flight
-        auto scan = [&](int j, int j1) {
-            for (; j < j1; j += BATCH) {
-                float4 q[BATCH];
-                int nn[BATCH];
-#pragma unroll
-                for (int t = 0; t < BATCH; ++t) {
-                    const int jj = min(j + t, N - 1);
-                    q[t] = spts[jj];
-                    nn[t] = sidx[jj];
-                }
-#pragma unroll
-                for (int t = 0; t < BATCH; ++t) {
-                    const float p[4] = {q[t].x, q[t].y, q[t].z, q[t].w};
-                    if (j + t < j1 && !(bq_dist<4>(c, c4.w, p, 3, false) > r2))
-                        atomicOr(&mrow[nn[t] >> 5], 1u << (nn[t] & 31));
-                }
-            }
-        };
-        if (!rec_finite(c4)) {
-            scan(0, N);
-        } else {
-            const float rr = sqrtf(r2 + ldexpf(c4.w + v[6], -16)) * 1.0001f +
-                             sqrtf(c4.w + v[6]) * 1e-6f;
-            int l[3], u[3];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                l[a] = cellc(c[a] - rr, a);
-                u[a] = cellc(c[a] + rr, a);
-            }
-            for (int z = l[2]; z <= u[2]; ++z)
-                for (int y = l[1]; y <= u[1]; ++y) {
-                    const int row = (z * G[1] + y) * G[0];
-                    scan(cstart[row + l[0]], cstart[row + u[0] + 1]);
-                }
-            scan(nfin, N);
-        }
-    }
-    __syncthreads();
-    if (stop == 3) return;
-
-    // 5. each lane's first K hits in index order (its mask words, lowest bit first) into its
-    // row of the LDS row buffer (rowbuf) or straight into its output row; then the rows out,
-    // one per wave step, coalesced: hits (rowbuf) and the padding
-    OT *rows = reinterpret_cast<OT *>(mask + MS * NT);  // [NT][K + 1] when rowbuf
-    const int KP = K + 1;
-    {
-        int cnt = 0;
-        OT first = (OT)N;
-        if (s < S) {
-            const unsigned *mrow = mask + tid * MS;
-            OT *dst = rowbuf ? rows + tid * KP : out + ((int64_t)b * S + s) * K;
-            for (int x = 0; x < NWD && cnt < K; ++x) {
-                unsigned wd = mrow[x];
-                while (wd != 0u && cnt < K) {
-                    const OT n = (OT)(x * 32 + __builtin_ctz(wd));
-                    if (cnt == 0) first = n;
-                    dst[cnt++] = n;
-                    wd &= wd - 1u;
-                }
-            }
-        }
-        nrow[tid] = cnt;
-        frow[tid] = (int)first;
-    }
-    __syncthreads();
-    for (int j = w; j < NT; j += WV) {
-        if (g0 + j >= S) break;
-        const int cj = nrow[j];
-        const OT fj = (OT)frow[j];
-        if (cj == 0 && lane == 0) atomicOr(&g_bq_errors, (unsigned)PN2_DEVERR_NO_NEIGHBOUR);
-        OT *ow = out + ((int64_t)b * S + g0 + j) * K;
-        if (rowbuf) {
-            for (int k = lane; k < K; k += 64) ow[k] = k < cj ? rows[j * KP + k] : fj;
-        } else {
-            for (int k = cj + lane; k < K; k += 64) ow[k] = fj;
-        }
-        if (out_cnt && lane == 0) out_cnt[(int64_t)b * S + g0 + j] = cj;
-    }
-}
-
 }  // namespace pn2
 
 using namespace pn2;
-
-// 1: launched; 0: not eligible (the scan kernel runs); <0: error
-template <typename OT>
-static int launch_bq_grid(const float *pp, const float *cp_, int64_t B, int64_t N, int64_t S,
-                          float r2, double radius, int64_t K, OT *out, int *cnt, hipStream_t st) {
-    const int64_t mode = tuning().bq_grid;
-    if (mode == 0) return 0;
-    if (mode == 1 && radius * 1000.0 > (double)tuning().bq_grid_rmax_milli) return 0;
-    if (N > 2048) return 0;  // mask words of a row across one wave's lanes
-    const int WV = tuning().bq_grid_waves == 4 ? 4 : 2;
-    const int NT = 64 * WV;
-    const int64_t ppt = (N + NT - 1) / NT;
-    if (ppt > 16) return 0;
-    size_t lds = bq_grid_lds((int)N, NT, (int)K + 1, (int)sizeof(OT));
-    int rowbuf = 1;
-    if (lds > (size_t)96 * 1024) {  // rows too long for LDS: hits straight to HBM
-        rowbuf = 0;
-        lds = bq_grid_lds((int)N, NT, 0, 0);
-    }
-    if (lds > (size_t)150 * 1024) return 0;
-    const int64_t nblk = B * ((S + NT - 1) / NT);
-    PN2_REQUIRE(nblk < (int64_t)1 << 31, "pn2_ball_query_f32: too many centroids");
-#define PN2_BQG(WW, PP)                                                                         \
-    do {                                                                                        \
-        static const hipError_t attr = hipFuncSetAttribute(                                    \
-            reinterpret_cast<const void *>(&ball_query_grid_kernel<WW, PP, OT>),               \
-            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);                           \
-        PN2_REQUIRE(attr == hipSuccess, "pn2_ball_query_f32: LDS attribute");                  \
-        hipLaunchKernelGGL((ball_query_grid_kernel<WW, PP, OT>), dim3((unsigned)nblk),          \
-                           dim3(64 * WW), lds, st, pp, cp_, (int)N, (int)S, r2, (int)K, out, cnt, rowbuf, \
-                           (int)tuning().bq_grid_stop);                                         \
-    } while (0)
-    const int P = ppt <= 4 ? 4 : ppt <= 8 ? 8 : 16;
-    if (WV == 4) {
-        if (P == 4) PN2_BQG(4, 4);
-        else if (P == 8) PN2_BQG(4, 8);
-        else PN2_BQG(4, 16);
-    } else {
-        if (P == 4) PN2_BQG(2, 4);
-        else if (P == 8) PN2_BQG(2, 8);
-        else PN2_BQG(2, 16);
-    }
-#undef PN2_BQG
-    PN2_LAUNCH_CHECK("ball_query_grid_kernel");
-    return 1;
-}
 
 template <int CP, int CC, typename OT>
 static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, int64_t S,
@@ -641,11 +318,6 @@ static int ball_query_impl(const float *pts_packed, const float *ctr_packed, int
     const float r2 = (float)(radius * radius);
     hipStream_t st = as_stream(stream);
     const int64_t cp = pn2_packed_stride(C);
-    if (C == 3 && cp == 4 && S * N * C >= 400) {
-        const int g = launch_bq_grid<OT>(pts_packed, ctr_packed, B, N, S, r2, radius, K, out_idx,
-                                         out_cnt, st);
-        if (g != 0) return g < 0 ? g : PN2_OK;
-    }
 #define PN2_BQ(CPV, CC) \
     if (cp == CPV && (CC == 0 || (C == CC && S * N * C >= 400))) \
         return launch_bq<CPV, CC, OT>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);

@@ -39,11 +39,6 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(bq_waves, 0)         /* ball query waves per workgroup (0: automatic, 8 or 16)       */ \
     X(bq_rowbuf_kb, 96)    /* largest LDS row buffer of the ball query (KB); bigger rows   */ \
                            /* are written straight to HBM (0: always)                      */ \
-    X(bq_grid, 0)          /* xyz ball query through a per-workgroup cell grid: 0 never,    */ \
-                           /* 1 when radius <= bq_grid_rmax_milli / 1000, 2 always          */ \
-    X(bq_grid_rmax_milli, 1000)                                                                \
-    X(bq_grid_waves, 0)    /* waves per grid workgroup (0: automatic, 2 or 4)               */ \
-    X(bq_grid_stop, 0)     /* timing only: the grid kernel stops after step 1, 2 or 3       */ \
     X(fps_threads, 0)      /* FPS block shape threads x points per thread (0: automatic)   */ \
     X(fps_ppt, 0)                                                                              \
     X(fps_cull, 0)         /* 1: culled FPS for xyz clouds (0: the index-ordered kernel)    */ \

@@ -6,8 +6,7 @@ The product path reads one environment variable, once, at import:
 
 Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_set``:
 ``mlp_f32``, ``chain_prepass``, ``compact``, ``compact_pool``, ``compact_stages``,
-``bq_waves``, ``bq_rowbuf_kb``, ``bq_grid``, ``bq_grid_rmax_milli``, ``bq_grid_waves``,
-``fps_threads``, ``fps_ppt``, ``fps_cull``, ``dense_maxntc``,
+``bq_waves``, ``bq_rowbuf_kb``, ``fps_threads``, ``fps_ppt``, ``fps_cull``, ``dense_maxntc``,
 ``dense_minwg``, ``dense_wide_minwg``, ``dense_lds``, ``dense_lds_stages``, ``dense_lds_xcd2d``,
 ``dense_lds_tile``; csrc/pn2_internal.h documents each) and these host-side ones:
 
