@@ -23,8 +23,8 @@ python - <<'PY'
 import json
 for f in ["bench_default"] + ["bench_k20_%d" % i for i in (1, 2, 3)]:
     d = json.load(open("gpurun_out/end/%s.json" % f))
-    print(f, d["value"], d["ms_per_step"], d.get("eager_value"), d["roofline"]["frac"],
-          (d.get("cpu_baseline") or {}).get("value"))
+    print(f, d["value"], d["ms_per_step"], (d.get("value_settled") or {}).get("value"),
+          d.get("eager_value"), d["roofline"]["frac"], (d.get("cpu_baseline") or {}).get("value"))
 PY
 rm -rf $OUT/prof_pipe $OUT/prof_eager
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_pipe -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timer > $OUT/prof_pipe.log 2>&1
