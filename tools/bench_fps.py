@@ -1,7 +1,7 @@
 """Sweep the FPS kernel's block shapes (tuning keys fps_threads / fps_ppt) on the GPU for the
 BASELINE geometries, checking every variant against the CPU oracle first.  Prints one line per
 (shape, variant): microseconds per launch and per serial iteration.
-    python tools/bench_fps.py [--default-only] [--tag NAME]
+    python tools/bench_fps.py [--default-only] [--tag NAME] [--shapes=ssg_sa1,...] [--variants=256x4,...]
 (PN2_TUNING=lib=<path> times another build of the library.)"""
 import json
 import os
@@ -44,7 +44,10 @@ def main():
     only_default = "--default-only" in sys.argv
     tag = sys.argv[sys.argv.index("--tag") + 1] if "--tag" in sys.argv else ""
     res = []
+    shp = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--shapes=")]
     for name, B, N, C, S, kind in SHAPES:
+        if shp and name not in shp[0]:
+            continue
         x = cases.as_layout(cases.cloud(kind, B, N, 5), "strided")
         xd = x.permute(0, 2, 1).contiguous().to(dev).permute(0, 2, 1)
         start = torch.randint(0, N, (B,), generator=torch.Generator().manual_seed(1))
