@@ -989,10 +989,15 @@ static int dispatch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64
     if (N <= 256) return launch_fps<64, 4, CM, FIXED>(A);
     // measured on MI355X (tools/bench_fps.py): two points per lane and 4-16 waves win until
     // the per-wave register set grows; past 2048 points the block is capped at 1024 threads.
-    // Up to 1024 points: 4 waves of 4 points -- alone on the chip it ties 512 x 2 (SSG sa1
-    // 176 us either way), in the pipeline (FPS beside the chains, sharing their SIMDs) its
-    // smaller footprint reads +1.2 % (SSG, 3 interleaved rounds, sa1 and sa2 both at 256 x 4)
-    if (N <= 1024) return launch_fps<256, 4, CM, FIXED>(A);
+    // Up to 1024 points (tuning fps_mid): alone on the chip 8 waves of 2 points are fastest
+    // (r04, interleaved x3: SSG sa1 154 vs 178 us at 256 x 4, sa2 43.0 vs 49.4; the eager
+    // forward +6.5 %); in the pipelines, beside the chains on the same SIMDs, 4 waves of 4
+    // points read ~2 % better (K = 100, tools/gpu_r04ab.sh), so pn2/pipeline.py selects that
+    // for its geometry
+    if (N <= 1024) {
+        if (tuning().fps_mid == 256) return launch_fps<256, 4, CM, FIXED>(A);
+        return launch_fps<512, 2, CM, FIXED>(A);
+    }
     if (N <= 2048) return launch_fps<1024, 2, CM, FIXED>(A);
     if (N <= 4096) return launch_fps<1024, 4, CM, FIXED>(A);
     if constexpr (CAP >= 8192)

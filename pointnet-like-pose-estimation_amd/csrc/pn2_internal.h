@@ -41,6 +41,9 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
                            /* are written straight to HBM (0: always)                      */ \
     X(fps_threads, 0)      /* FPS block shape threads x points per thread (0: automatic)   */ \
     X(fps_ppt, 0)                                                                              \
+    X(fps_mid, 512)        /* automatic FPS block for 256 < N <= 1024: 512 threads x 2      */ \
+                           /* points (fastest alone: the eager forward) or 256 x 4 (the     */ \
+                           /* pipelines' geometry, beside the chains: pn2/pipeline.py)      */ \
     X(fps_cull, 0)         /* 1: culled FPS for xyz clouds (0: the index-ordered kernel)    */ \
                            /* (NT*100 + Q*10 + PPC: force a compiled culled shape)          */ \
     X(dense_maxntc, 2)     /* widest 32-column tile count of the 4-wave dense layer         */ \

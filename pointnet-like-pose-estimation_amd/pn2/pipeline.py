@@ -217,6 +217,13 @@ class PipelinedForward:
         one after the other.  The copy keeps x's layout (the packed squared norms follow the
         reference's layout-dependent summation order), and every start is still drawn in layer
         order before any launch."""
+        mid = int(tuning.get("pipe_fps_mid"))
+        if mid:  # the FPS block shape measured best beside the chains (csrc/fps.hip)
+            with tuning.override(fps_mid=mid):
+                return self._fps_chain_body(x)
+        return self._fps_chain_body(x)
+
+    def _fps_chain_body(self, x):
         B, _, N = x.shape
         dev = x.device
         chains, cur = [], []

@@ -6,7 +6,7 @@ The product path reads one environment variable, once, at import:
 
 Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_set``:
 ``mlp_f32``, ``chain_prepass``, ``compact``, ``compact_pool``, ``compact_stages``,
-``bq_waves``, ``bq_rowbuf_kb``, ``fps_threads``, ``fps_ppt``, ``fps_cull``, ``dense_maxntc``,
+``bq_waves``, ``bq_rowbuf_kb``, ``fps_threads``, ``fps_ppt``, ``fps_mid``, ``fps_cull``, ``dense_maxntc``,
 ``dense_minwg``, ``dense_wide_minwg``, ``dense_lds``, ``dense_lds_stages``, ``dense_lds_xcd2d``,
 ``dense_lds_tile``; csrc/pn2_internal.h documents each) and these host-side ones:
 
@@ -25,6 +25,8 @@ Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_s
                      bench's --force-rccl measurement of the collective's cost on one GPU)
     geometry_bq      1: the pipeline's geometry stream runs the ball queries after the FPS;
                      0: only the FPS, each batch's forward (compute stream) queries
+    pipe_fps_mid     the kernel key fps_mid while the pipelines take their geometry (256: the
+                     FPS block of 4 waves x 4 points beside the chains; 0: leave fps_mid)
 
 Unknown keys are an error.  ``override(**kw)`` changes keys for the duration of a ``with``
 block (tests).  Every default is the measured best.
@@ -34,6 +36,7 @@ import os
 
 HOST_DEFAULTS = {
     "lib": "",
+    "pipe_fps_mid": 256,
     "tail_prio": 0,
     "heads_on_compute": 0,
     "pipe_split_last": 0,

@@ -247,3 +247,19 @@ def test_index_points_out_of_range_is_nan_and_flagged():
     assert torch.equal(got[0, 0], pts[0, 0])
     with pytest.raises(IndexError, match="out of range"):
         pn2.check_device_errors()
+
+
+@pytest.mark.parametrize("mid", [256, 512])
+@pytest.mark.parametrize("C,N", [(3, 1024), (3, 512), (3, 300), (10, 1024), (6, 777)])
+def test_fps_mid_shapes_exact(mid, C, N):
+    """Both automatic FPS blocks for 256 < N <= 1024 (tuning fps_mid: 512 x 2, the eager
+    default; 256 x 4, the pipelines' geometry) give the oracle's indices."""
+    from pn2 import tuning
+    gen = torch.Generator().manual_seed(77 + C + N)
+    B, S = 4, min(N, 256)
+    p = cases.as_layout(torch.randn(B, N, C, generator=gen), "strided")
+    start = torch.randint(0, N, (B,), generator=gen)
+    want = oracle.farthest_point_sample(p, S, start)
+    with tuning.override(fps_mid=mid):
+        idx, newp, cpk, ppk = torch.ops.pn2.fps(_to_dev_view(p), S, start.to(DEV))
+    np.testing.assert_array_equal(idx.cpu().numpy(), want)
