@@ -252,10 +252,11 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
                      int64_t C, float r2, int64_t K, OT *out, int *cnt, hipStream_t st) {
     const int64_t nblk = B * ((S + 63) / 64);
     PN2_REQUIRE(nblk < (int64_t)1 << 31, "pn2_ball_query_f32: too many centroids");
-    // waves per workgroup: 16 for long xyz clouds (more segments in flight), else 8
-    // (profiles/r02_bq/bq_modes.txt); tuning bq_waves = 8 | 16 overrides
+    // waves per workgroup: bq_waves = 16 (the default: alone on the chip more segments in
+    // flight win, SSG eager +1 %, r04) or 8; 0 = the pipelines' choice, 16 for long xyz clouds
+    // only (profiles/r02_bq/bq_modes.txt).  Clouds with extra channels keep 8 (LDS budget)
     int P = (CP == 4 && N >= 2048) ? 16 : 8;
-    if (tuning().bq_waves) P = tuning().bq_waves == 16 ? 16 : 8;
+    if (tuning().bq_waves) P = (tuning().bq_waves == 16 && CP == 4) ? 16 : 8;
     // words per segment: a round stages up to P*32*nw records (<= 64 per wave beyond xyz)
     const int64_t per_wave = (N + P - 1) / P;
     int nw = per_wave <= 32 ? 1 : per_wave <= 64 ? 2 : 4;

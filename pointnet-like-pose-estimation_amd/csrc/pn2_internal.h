@@ -36,20 +36,24 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(compact, 1)          /* 0: no compact neighbourhoods (every padded row computed)     */ \
     X(compact_pool, 16)     /* LDS pool rows of compact chain launches (0: automatic)       */ \
     X(compact_stages, 3)   /* weight-ring stages of compact chain launches (2 or 3)        */ \
-    X(bq_waves, 0)         /* ball query waves per workgroup (0: automatic, 8 or 16)       */ \
+    X(bq_waves, 16)        /* ball query waves per workgroup (8 or 16; 0: 16 for xyz clouds  */ \
+                           /* of >= 2048 points, else 8 -- the pipelines' choice)           */ \
     X(bq_rowbuf_kb, 96)    /* largest LDS row buffer of the ball query (KB); bigger rows   */ \
                            /* are written straight to HBM (0: always)                      */ \
     X(fps_threads, 0)      /* FPS block shape threads x points per thread (0: automatic)   */ \
     X(fps_ppt, 0)                                                                              \
     X(fps_mid, 512)        /* automatic FPS block for 256 < N <= 1024: 512 threads x 2      */ \
                            /* points (fastest alone: the eager forward) or 256 x 4 (the     */ \
-                           /* pipelines' geometry, beside the chains: pn2/pipeline.py)      */ \
+                           /* pipelines' geometry, beside the chains)                       */ \
     X(fps_cull, 0)         /* 1: culled FPS for xyz clouds (0: the index-ordered kernel)    */ \
                            /* (NT*100 + Q*10 + PPC: force a compiled culled shape)          */ \
     X(dense_maxntc, 2)     /* widest 32-column tile count of the 4-wave dense layer         */ \
     X(dense_minwg, 256)    /* workgroups a wider dense tile must still leave                 */ \
     X(dense_wide_minwg, 512) /* workgroups the 256 x 128 dense tile must leave              */ \
-    X(dense_lds, 0)        /* 1: LDS-staged dense kernel (faster alone, slower pipelined)   */ \
+    X(dense_lds, 1)        /* 1: LDS-staged dense kernel for layers of >= dense_lds_mincin   */ \
+                           /* input channels (faster alone: the eager forward; the          */ \
+                           /* pipelines run with 0, pn2/tuning.py PIPELINE_PROFILE)         */ \
+    X(dense_lds_mincin, 0)                                                                     \
     X(dense_lds_stages, 3) /* ring stages of the LDS-staged dense kernel (3 or 4)            */ \
     X(dense_lds_xcd2d, 0)  /* 1: XCD rectangles of row blocks x column tiles                */ \
     X(dense_lds_tile, 0)   /* LDS-staged dense tile WR*10+NTW (82, 44, 42, 22; 0: auto)      */

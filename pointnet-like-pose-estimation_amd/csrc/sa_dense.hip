@@ -762,6 +762,10 @@ static const int kLdsTiles[] = {82, 44, 42, 22};
 
 static int dense_lds_tile(const DenseSplitArgs &A) {
     if (!tuning().dense_lds || !A.vec) return 0;
+    // tuning dense_lds_mincin keeps narrower layers on the register-staged kernel (default 0:
+    // none -- SSG eager 67.6k at 0 or 128 vs 66.6k at 256, PointNet-v1 equal or faster,
+    // tools/gpu_r04af.sh)
+    if ((A.mode == 0 ? A.cin : A.D) < tuning().dense_lds_mincin) return 0;
     const bool ok = A.mode == 0 ? (A.cin % 32 == 0 && A.kb * 16 == A.cin && A.rs % 4 == 0 &&
                                    ((uintptr_t)A.rows & 15) == 0)
                                 : (A.feat && A.D > 0 && A.D % 32 == 0 && A.kb == 1 + A.D / 16 &&

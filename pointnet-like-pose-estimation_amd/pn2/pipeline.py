@@ -217,11 +217,8 @@ class PipelinedForward:
         one after the other.  The copy keeps x's layout (the packed squared norms follow the
         reference's layout-dependent summation order), and every start is still drawn in layer
         order before any launch."""
-        mid = int(tuning.get("pipe_fps_mid"))
-        if mid:  # the FPS block shape measured best beside the chains (csrc/fps.hip)
-            with tuning.override(fps_mid=mid):
-                return self._fps_chain_body(x)
-        return self._fps_chain_body(x)
+        with tuning.pipeline_profile():  # the launch choices measured best beside the chains
+            return self._fps_chain_body(x)
 
     def _fps_chain_body(self, x):
         B, _, N = x.shape
@@ -298,7 +295,8 @@ class PipelinedForward:
         if use_tail and self.sas:
             handle = self.sas[-1].register_forward_hook(self._to_tail(tail))
         try:
-            self._run(batches, extras, post, geo, main, outs)
+            with tuning.pipeline_profile():
+                self._run(batches, extras, post, geo, main, outs)
         finally:
             if handle is not None:
                 handle.remove()
@@ -574,9 +572,10 @@ class GraphedPipeline(PipelinedForward):
         """New sa / head graphs for every batch slot after a parameter change (their kernels
         read the parameters' memory); the geometry graphs read only coordinates and draws, and
         are kept."""
-        for grp in self._slots:
-            grp.halves = [self._capture_forward(sl.x, extra, dev, *self._half_entries(grp, h))
-                          for h, sl in enumerate(grp.halves)]
+        with tuning.pipeline_profile():
+            for grp in self._slots:
+                grp.halves = [self._capture_forward(sl.x, extra, dev, *self._half_entries(grp, h))
+                              for h, sl in enumerate(grp.halves)]
 
     def _capture_forward(self, x, extra, dev, entries, geo):
         sl = _Slot()
@@ -651,8 +650,9 @@ class GraphedPipeline(PipelinedForward):
                 outs = self._run_eager(batches[:1], None if extras is None else extras[:1],
                                        post, False)
             self._draws = draws
-            self._slots = [self._capture(batches[0], extra_of(0), dev, draws)
-                           for _ in range(self.ngroups)]
+            with tuning.pipeline_profile():
+                self._slots = [self._capture(batches[0], extra_of(0), dev, draws)
+                               for _ in range(self.ngroups)]
             self._key = sig
             self._pkey = self._params.key()  # capture allocations do not touch parameters
             # replay every captured graph once now, in dependency order on this stream (start

@@ -25,8 +25,10 @@ Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_s
                      bench's --force-rccl measurement of the collective's cost on one GPU)
     geometry_bq      1: the pipeline's geometry stream runs the ball queries after the FPS;
                      0: only the FPS, each batch's forward (compute stream) queries
-    pipe_fps_mid     the kernel key fps_mid while the pipelines take their geometry (256: the
-                     FPS block of 4 waves x 4 points beside the chains; 0: leave fps_mid)
+    pipe_profile     1: the pipelines (pn2.pipeline) capture and run their kernels under
+                     PIPELINE_PROFILE -- the launch choices measured best beside each other's
+                     kernels, where the kernel defaults are the ones measured best alone (the
+                     eager forward, GraphedForward); 0: the defaults everywhere
 
 Unknown keys are an error.  ``override(**kw)`` changes keys for the duration of a ``with``
 block (tests).  Every default is the measured best.
@@ -36,7 +38,7 @@ import os
 
 HOST_DEFAULTS = {
     "lib": "",
-    "pipe_fps_mid": 256,
+    "pipe_profile": 1,
     "tail_prio": 0,
     "heads_on_compute": 0,
     "pipe_split_last": 0,
@@ -62,6 +64,21 @@ def _parse(text):
 _ENV = _parse(os.environ.get("PN2_TUNING", ""))
 _host = dict(HOST_DEFAULTS)
 _host.update({k: v for k, v in _ENV.items() if k in HOST_DEFAULTS})
+
+
+# Kernel keys the pipelines set while they capture / run: the FPS block of 4
+# waves x 4 points, the register-staged dense kernel and 8-wave ball-query workgroups (for
+# clouds below 2048 points) -- each faster alone in the other form, slower beside the chains.
+PIPELINE_PROFILE = {"fps_mid": 256, "dense_lds": 0, "bq_waves": 0}
+
+
+def pipeline_profile():
+    """Context: PIPELINE_PROFILE applied (when pipe_profile is on), then restored.  The keys
+    are process-wide: a forward on another host thread meanwhile gets the same (exact) kernels
+    in their pipelined forms."""
+    if not _host["pipe_profile"]:
+        return contextlib.nullcontext()
+    return override(**PIPELINE_PROFILE)
 
 
 def get(key):

@@ -91,7 +91,7 @@ def test_tuning_switch_keys():
     for k in ("mlp_f32", "compact", "bq_waves", "bq_rowbuf_kb", "fps_threads", "fps_ppt", "dense_lds"):
         assert k in keys
     v = ctypes.c_int64(-1)
-    assert L.pn2_tuning_get(b"dense_lds", ctypes.byref(v)) == 0 and v.value == 0
+    assert L.pn2_tuning_get(b"dense_lds", ctypes.byref(v)) == 0 and v.value == 1
     assert L.pn2_tuning_set(b"no_such_key", 1) != 0
     with tuning.override(fps_threads=512, tail_streams=2):
         assert tuning.kernel("fps_threads") == 512 and tuning.get("tail_streams") == 2

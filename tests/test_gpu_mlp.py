@@ -265,7 +265,7 @@ def test_dense_lds_matches_register_staged(case, prec):
     f = feat.permute(0, 2, 1).contiguous().to(DEV)
     outs = []
     for lds in (1, 0):
-        with torch.no_grad(), pn2.mlp_precision(prec), tuning.override(dense_lds=lds):
+        with torch.no_grad(), pn2.mlp_precision(prec), tuning.override(dense_lds=lds, dense_lds_mincin=0):
             outs.append(sa(x, f)[1].cpu().numpy())
     np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
     if prec == "fp32":
@@ -285,7 +285,7 @@ def test_dense_lds_rows_source_v1():
     x = cases.cloud("uniform3", 8, 1024, 9).permute(0, 2, 1).contiguous().to(DEV)
     outs = []
     for lds in (1, 0):
-        with torch.no_grad(), tuning.override(dense_lds=lds):
+        with torch.no_grad(), tuning.override(dense_lds=lds, dense_lds_mincin=0):
             o = model(x)
             outs.append([t.cpu().numpy() for t in (o if isinstance(o, tuple) else (o,)) if t is not None])
     for a, b in zip(*outs):

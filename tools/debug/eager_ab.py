@@ -29,6 +29,10 @@ VARIANTS = [
     ("lds_bq16", dict(dense_lds=1, bq_waves=16)),
     ("lds_bq16_mw512", dict(dense_lds=1, bq_waves=16, dense_minwg=512)),
 ]
+if os.environ.get("EAGER_AB_SET") == "profile":
+    VARIANTS = [("default", {}), ("mincin0", dict(dense_lds_mincin=0)), ("mincin128", dict(dense_lds_mincin=128)),
+                ("pipeline_profile", dict(fps_mid=256, dense_lds=0, bq_waves=0)),
+                ("no_lds", dict(dense_lds=0)), ("bq8", dict(bq_waves=0))]
 if os.environ.get("EAGER_AB_SET") == "short":
     VARIANTS = [v for v in VARIANTS if v[0] in ("default", "dense_lds", "bq16", "lds_bq16", "lds_bq16_mw512")]
 
