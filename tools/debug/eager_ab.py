@@ -33,6 +33,12 @@ if os.environ.get("EAGER_AB_SET") == "profile":
     VARIANTS = [("default", {}), ("mincin0", dict(dense_lds_mincin=0)), ("mincin128", dict(dense_lds_mincin=128)),
                 ("pipeline_profile", dict(fps_mid=256, dense_lds=0, bq_waves=0)),
                 ("no_lds", dict(dense_lds=0)), ("bq8", dict(bq_waves=0))]
+if os.environ.get("EAGER_AB_SET") == "more":
+    VARIANTS = [("default", {}), ("lds_st4", dict(dense_lds_stages=4)), ("lds_xcd2d", dict(dense_lds_xcd2d=1)),
+                ("tile44", dict(dense_lds_tile=44)), ("tile42", dict(dense_lds_tile=42)),
+                ("tile22", dict(dense_lds_tile=22)), ("tile82", dict(dense_lds_tile=82)),
+                ("minwg512", dict(dense_minwg=512)), ("no_prepass", dict(chain_prepass=0)),
+                ("rowbuf0", dict(bq_rowbuf_kb=0))]
 if os.environ.get("EAGER_AB_SET") == "short":
     VARIANTS = [v for v in VARIANTS if v[0] in ("default", "dense_lds", "bq16", "lds_bq16", "lds_bq16_mw512")]
 
