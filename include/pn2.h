@@ -58,7 +58,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 12
+#define PN2_ABI_VERSION 13
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -85,6 +85,11 @@ int pn2_device_errors(int clear, uint32_t *bits);
 int pn2_tuning_get(const char *key, int64_t *value);
 int pn2_tuning_set(const char *key, int64_t value);
 const char *pn2_tuning_keys(void);
+/* pn2_tuning_local(1): this host thread gets its own copy of the keys (taken from the
+ * process-wide values at the outermost enter); pn2_tuning_get/set and every launch on this
+ * thread then use the copy, other threads are unaffected; pn2_tuning_local(0) leaves (nested
+ * enters count).  pn2.pipeline captures its graphs in this mode under its own launch profile. */
+int pn2_tuning_local(int enter);
 
 /* Packed point layout used by the ball query: [B][N][cp] float32, cp = pn2_packed_stride(C),
  * holding the C coordinates, then ssq = torch.sum(p**2,-1) computed with the reference's

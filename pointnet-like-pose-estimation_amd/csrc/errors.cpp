@@ -1,5 +1,6 @@
 // errors.cpp -- the pn2 C ABI's library state: the thread-local error message and the
-// process-wide kernel-selection tuning (pn2_internal.h PN2_TUNING_KEYS).
+// kernel-selection tuning (pn2_internal.h PN2_TUNING_KEYS): process-wide, or a thread's own
+// copy between pn2_tuning_local(1) and pn2_tuning_local(0).
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -18,8 +19,22 @@ int set_error(int code, const char *fmt, ...) {
 }
 
 static Tuning g_tuning;
-const Tuning &tuning() { return g_tuning; }
+// pn2_tuning_local: this thread's own copy of the keys while depth > 0
+static thread_local Tuning t_tuning;
+static thread_local int t_depth = 0;
+static Tuning &active() { return t_depth > 0 ? t_tuning : g_tuning; }
+const Tuning &tuning() { return t_depth > 0 ? t_tuning : g_tuning; }
 }  // namespace pn2
+
+extern "C" int pn2_tuning_local(int enter) {
+    if (enter) {
+        if (pn2::t_depth++ == 0) pn2::t_tuning = pn2::g_tuning;
+        return PN2_OK;
+    }
+    PN2_REQUIRE(pn2::t_depth > 0, "pn2_tuning_local: leave without enter");
+    --pn2::t_depth;
+    return PN2_OK;
+}
 
 extern "C" const char *pn2_last_error(void) { return pn2::g_msg; }
 extern "C" int pn2_abi_version(void) { return PN2_ABI_VERSION; }
@@ -37,7 +52,7 @@ extern "C" int pn2_tuning_get(const char *key, int64_t *value) {
     PN2_REQUIRE(key && value, "pn2_tuning_get: null pointer");
 #define PN2_TUNING_GET(name, dflt)                 \
     if (strcmp(key, #name) == 0) {                 \
-        *value = pn2::g_tuning.name;               \
+        *value = pn2::active().name;               \
         return PN2_OK;                             \
     }
     PN2_TUNING_KEYS(PN2_TUNING_GET)
@@ -49,7 +64,7 @@ extern "C" int pn2_tuning_set(const char *key, int64_t value) {
     PN2_REQUIRE(key, "pn2_tuning_set: null pointer");
 #define PN2_TUNING_SET(name, dflt)                 \
     if (strcmp(key, #name) == 0) {                 \
-        pn2::g_tuning.name = value;                \
+        pn2::active().name = value;                \
         return PN2_OK;                             \
     }
     PN2_TUNING_KEYS(PN2_TUNING_SET)

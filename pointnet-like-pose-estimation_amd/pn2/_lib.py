@@ -110,13 +110,14 @@ SIGNATURES = {
     "pn2_tuning_get": (_int, [ctypes.c_char_p, ctypes.POINTER(_i64)]),
     "pn2_tuning_set": (_int, [ctypes.c_char_p, _i64]),
     "pn2_tuning_keys": (ctypes.c_char_p, []),
+    "pn2_tuning_local": (_int, [_int]),
     "pn2_device_errors": (_int, [_int, ctypes.POINTER(ctypes.c_uint32)]),
     "pn2_fc_tail_workspace_bytes": (_i64, [_i64, _i64, _i64]),
     "pn2_fc_tail_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64,
                                _int, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 _lib = None
 
 

@@ -72,13 +72,28 @@ _host.update({k: v for k, v in _ENV.items() if k in HOST_DEFAULTS})
 PIPELINE_PROFILE = {"fps_mid": 256, "dense_lds": 0, "bq_waves": 0}
 
 
+@contextlib.contextmanager
+def local():
+    """Context: this host thread's own copy of the kernel keys (pn2_tuning_local); changes
+    inside it do not reach other threads and end with it."""
+    from . import _lib
+    L = _lib.load()
+    _lib.check(L.pn2_tuning_local(1), "pn2_tuning_local")
+    try:
+        yield
+    finally:
+        _lib.check(L.pn2_tuning_local(0), "pn2_tuning_local")
+
+
+@contextlib.contextmanager
 def pipeline_profile():
-    """Context: PIPELINE_PROFILE applied (when pipe_profile is on), then restored.  The keys
-    are process-wide: a forward on another host thread meanwhile gets the same (exact) kernels
-    in their pipelined forms."""
+    """Context: PIPELINE_PROFILE applied (when pipe_profile is on) on this thread's own copy of
+    the keys -- a forward on another host thread meanwhile keeps the defaults."""
     if not _host["pipe_profile"]:
-        return contextlib.nullcontext()
-    return override(**PIPELINE_PROFILE)
+        yield
+        return
+    with local(), override(**PIPELINE_PROFILE):
+        yield
 
 
 def get(key):

@@ -154,3 +154,32 @@ def test_io_library_exports_every_declared_symbol():
     assert L.pn2io_abi_version() == data.ABI_VERSION
     rc = L.pn2io_read_csv_f64(b"/nonexistent/x.txt", b",", 3, 10, None, None)
     assert rc == -4 and b"bad argument" in L.pn2io_last_error()
+
+
+def test_tuning_local_is_per_thread():
+    """pn2_tuning_local: a thread's own copy of the kernel keys (the pipelines capture under
+    their launch profile in it); other threads keep the process-wide values; nesting counts."""
+    import threading
+    from pn2 import tuning
+    base = tuning.kernel("fps_mid")
+    seen = {}
+    inside = threading.Event()
+    release = threading.Event()
+
+    def worker():
+        with tuning.pipeline_profile():
+            with tuning.local():  # nested enter keeps the copy
+                seen["nested"] = tuning.kernel("fps_mid")
+            seen["worker"] = tuning.kernel("fps_mid")
+            inside.set()
+            release.wait(10)
+        seen["after"] = tuning.kernel("fps_mid")
+
+    t = threading.Thread(target=worker)
+    t.start()
+    assert inside.wait(10)
+    seen["main"] = tuning.kernel("fps_mid")
+    release.set()
+    t.join(10)
+    assert seen == {"nested": 256, "worker": 256, "main": base, "after": base}
+    assert base == 512
