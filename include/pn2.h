@@ -8,11 +8,13 @@
  *   - is asynchronous on that stream and never synchronises the device, so it may be captured
  *     into a hipGraph;
  *   - returns PN2_OK (0) or a negative PN2_E* code; the message of the last failure on the
- *     calling thread is returned by pn2_last_error() (thread-local).  Besides it the library
- *     holds only the tuning parameters (set by tests / A/B tools) and the sticky device error
- *     word below, which kernels only ever OR into -- so calls are re-entrant across host
- *     threads, as the reference's concurrent-inference demo
- *     /root/reference/mutilthreading/predict_test.py:44-63 requires.
+ *     calling thread is returned by pn2_last_error() (thread-local).
+ *   - is re-entrant across host threads, as the reference's concurrent-inference demo
+ *     /root/reference/mutilthreading/predict_test.py:44-63 requires: besides the caller's
+ *     buffers the library holds only thread-local state (the error message, a thread's tuning
+ *     copy, a thread's device error slots), the process-wide tuning keys (one atomic word per
+ *     key) and the process-wide default error slot (kernels only OR into it; its reads are
+ *     serialised).
  *
  * Reference interfaces replaced (file:line in /root/reference):
  *   pn2_fps_f32            farthest_point_sample            model/pointnet2_utils.py:47-68
@@ -58,32 +60,44 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 13
+#define PN2_ABI_VERSION 14
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
 
-/* Device error word: conditions under which the reference raises but a kernel cannot.  The
+/* Device error slots: conditions under which the reference raises but a kernel cannot.  The
  * kernels stay in bounds (clamped or NaN outputs, documented per entry point) and OR a bit into
- * a per-device word; pn2_device_errors reads it (synchronously: hipDeviceSynchronize, so every
- * stream's work is done) and, when `clear` != 0, clears it in the same device atomic (a bit
- * raised meanwhile is never lost).  pn2.check_device_errors() raises IndexError.
+ * the device error slot of the host thread that launched them:
  *   PN2_DEVERR_NO_NEIGHBOUR  a ball-query centroid had no point within the radius (its row is
  *                            padded with N, pointnet2_utils.py:85-89; the reference's next
  *                            index_points raises IndexError); the SA kernels read point 0 there
  *   PN2_DEVERR_INDEX         pn2_index_points_f32 / pn2_group_f32 got an index outside [-N, N)
- *                            (the element is NaN) */
+ *                            (the element is NaN)
+ * pn2_error_slot_set(slot): from now on, launches by the calling thread on the current device
+ * raise into `slot` -- two caller-owned, zeroed uint32 DEVICE words ([0] the bits, [1] scratch
+ * for the take) that must outlive every launch and captured graph that uses them (a graph
+ * raises into the slot of the thread that captured it).  NULL: back to the process-wide
+ * default slot, which every thread without a slot of its own shares.
+ * pn2_error_slot_take: the calling thread's slot (on the current device), taken -- read and,
+ * when `clear` != 0, reset in ONE device atomic, so a bit raised meanwhile is never lost --
+ * stream-ordered on `stream`, which it then waits for.
+ * pn2_device_errors: the same take after hipDeviceSynchronize (every stream's work done).
+ * pn2.check_device_errors() gives each (thread, device) its own slot and raises IndexError. */
 #define PN2_DEVERR_NO_NEIGHBOUR 1u
 #define PN2_DEVERR_INDEX 2u
+int pn2_error_slot_set(uint32_t *slot);
+int pn2_error_slot_take(int clear, uint32_t *bits, void *stream);
 int pn2_device_errors(int clear, uint32_t *bits);
 
-/* Kernel-selection tuning: process-wide int64 parameters of the launch choices (which kernel
- * family, tile widths, block shapes).  The defaults are the measured best and the library never
- * reads the environment; tests and A/B tools change them (pn2/tuning.py applies the one
- * PN2_TUNING="key=value,..." variable at load).  Change them only while no pn2 call is in
- * flight on another host thread.  Keys: pn2_tuning_keys() (space-separated). */
+/* Kernel-selection tuning: int64 parameters of the launch choices (which kernel family, tile
+ * widths, block shapes).  The defaults are the measured best (pn2_tuning_default) and the
+ * library never reads the environment; tests and A/B tools change them (pn2/tuning.py applies
+ * the one PN2_TUNING="key=value,..." variable at load).  Process-wide keys are atomic words:
+ * a set on one thread while another launches is safe (the launch sees the old or the new value
+ * of each key).  Keys: pn2_tuning_keys() (space-separated). */
 int pn2_tuning_get(const char *key, int64_t *value);
 int pn2_tuning_set(const char *key, int64_t value);
+int pn2_tuning_default(const char *key, int64_t *value);
 const char *pn2_tuning_keys(void);
 /* pn2_tuning_local(1): this host thread gets its own copy of the keys (taken from the
  * process-wide values at the outermost enter); pn2_tuning_get/set and every launch on this

@@ -38,29 +38,6 @@
 
 namespace pn2 {
 
-// raised when a valid centroid has no point within the radius: its row is padded with index N
-// (the reference's out-of-range pad, pointnet2_utils.py:85-89, which makes its index_points
-// raise IndexError); the SA kernels clamp such indices instead of reading past the cloud
-__device__ unsigned g_bq_errors;
-
-// the word's value (and, with clear, its reset) in ONE device atomic: a bit that a kernel ORs in
-// between cannot be lost (a read followed by a separate clear could drop it)
-__device__ unsigned g_bq_snapshot;
-__global__ void bq_errors_take_kernel(int clear) {
-    g_bq_snapshot = clear ? atomicExch(&g_bq_errors, 0u) : atomicOr(&g_bq_errors, 0u);
-}
-
-int read_bq_errors(unsigned *bits, int clear) {
-    // every stream's work first: kernels still in flight on other streams may raise bits
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    hipLaunchKernelGGL(bq_errors_take_kernel, dim3(1), dim3(1), 0, 0, clear);
-    if (hipGetLastError() != hipSuccess) return -1;
-    unsigned v = 0;
-    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_bq_snapshot), sizeof(v)) != hipSuccess) return -1;
-    *bits = v;
-    return 0;
-}
-
 // CC > 0: the channel count is known at compile time (C = 3 xyz, C = 10 pose) and the shape is
 // not ATen's naive-bmm size; CC = 0: runtime C and the `small` flag.  NW bitmask words per
 // segment (TS = 32*NW points per wave per round).
@@ -101,7 +78,7 @@ __device__ __forceinline__ void bq_insert(unsigned &wd, float d, float r2) {
 template <int CP, int CC, int NW, int P, typename OT, bool ROWBUF>
 __global__ __launch_bounds__(64 * P) void ball_query_kernel(
     const float *__restrict__ pts, const float *__restrict__ ctr, int N, int S, int C_, float r2,
-    int K, int small_, OT *__restrict__ out, int *__restrict__ out_cnt) {
+    int K, int small_, OT *__restrict__ out, int *__restrict__ out_cnt, unsigned *__restrict__ err) {
     constexpr int TS = 32 * NW;
     constexpr int TV = P * TS * CP / 4;  // float4 per staged round
     __shared__ float4 tile[TV];
@@ -232,7 +209,10 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
         if (g0 + j >= S) break;
         const int cj = min(__builtin_amdgcn_readlane(total, j), K);
         const OT fj = cj > 0 ? (ROWBUF ? obuf[j * KP] : (OT)first[j]) : (OT)N;
-        if (cj == 0 && lane == 0) atomicOr(&g_bq_errors, (unsigned)PN2_DEVERR_NO_NEIGHBOUR);
+        // no point within the radius: the row is padded with index N (the reference's
+        // out-of-range pad, pointnet2_utils.py:85-89, which makes its index_points raise
+        // IndexError); the SA kernels clamp such indices instead of reading past the cloud
+        if (cj == 0 && lane == 0) atomicOr(err, (unsigned)PN2_DEVERR_NO_NEIGHBOUR);
         OT *o = out + ((int64_t)b * S + g0 + j) * K;
         if constexpr (ROWBUF) {
             for (int k = lane; k < K; k += 64) o[k] = k < cj ? obuf[j * KP + k] : fj;
@@ -267,6 +247,8 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
     const size_t obytes = (size_t)64 * (K + 1) * sizeof(OT);
     const int64_t rb_kb = tuning().bq_rowbuf_kb < 96 ? tuning().bq_rowbuf_kb : 96;
     const bool rowbuf = obytes <= (size_t)rb_kb * 1024;
+    unsigned *err = error_word();
+    PN2_REQUIRE(err, "pn2_ball_query_f32: no device error slot");
 #define PN2_BQ_L2(NW, PP, RB)                                                                          \
     do {                                                                                               \
         static const hipError_t attr = hipFuncSetAttribute(                                           \
@@ -275,7 +257,7 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
         PN2_REQUIRE(attr == hipSuccess, "pn2_ball_query_f32: LDS attribute");                         \
         hipLaunchKernelGGL((ball_query_kernel<CP, CC, NW, PP, OT, RB>), dim3((unsigned)nblk),        \
                            dim3(64 * PP), RB ? obytes : 0, st, pp, cp_, (int)N, (int)S, (int)C, r2,   \
-                           (int)K, sm, out, cnt);                                                      \
+                           (int)K, sm, out, cnt, err);                                                 \
     } while (0)
 #define PN2_BQ_L(NW, PP)                    \
     do {                                    \

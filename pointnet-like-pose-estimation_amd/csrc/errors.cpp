@@ -1,9 +1,18 @@
-// errors.cpp -- the pn2 C ABI's library state: the thread-local error message and the
-// kernel-selection tuning (pn2_internal.h PN2_TUNING_KEYS): process-wide, or a thread's own
-// copy between pn2_tuning_local(1) and pn2_tuning_local(0).
+// errors.cpp -- the pn2 C ABI's library state, all of it safe under concurrent host threads
+// (the reference's /root/reference/mutilthreading/predict_test.py:44-63 runs four heads from four
+// threads on one device):
+//   - the error message of the last failure: thread-local;
+//   - the kernel-selection tuning (pn2_internal.h PN2_TUNING_KEYS): one atomic word per key
+//     process-wide (a launch reads a consistent snapshot of each key, never a torn value), or a
+//     thread's own copy between pn2_tuning_local(1) and pn2_tuning_local(0);
+//   - the device error slots: each thread's own slot per device (pn2_error_slot_set), or the
+//     process-wide default slot, whose reads are serialised by a host mutex.
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <atomic>
+#include <mutex>
 
 #include "pn2_internal.h"
 
@@ -18,17 +27,73 @@ int set_error(int code, const char *fmt, ...) {
     return code;
 }
 
-static Tuning g_tuning;
+// process-wide keys: relaxed atomics (a key is one independent value; no ordering between keys
+// is promised -- change them while no launch depends on two of them changing together)
+struct SharedTuning {
+#define PN2_TUNING_ATOMIC(name, dflt) std::atomic<int64_t> name{dflt};
+    PN2_TUNING_KEYS(PN2_TUNING_ATOMIC)
+#undef PN2_TUNING_ATOMIC
+};
+static SharedTuning g_tuning;
 // pn2_tuning_local: this thread's own copy of the keys while depth > 0
 static thread_local Tuning t_tuning;
 static thread_local int t_depth = 0;
-static Tuning &active() { return t_depth > 0 ? t_tuning : g_tuning; }
-const Tuning &tuning() { return t_depth > 0 ? t_tuning : g_tuning; }
+
+static Tuning shared_snapshot() {
+    Tuning t;
+#define PN2_TUNING_LOAD(name, dflt) t.name = g_tuning.name.load(std::memory_order_relaxed);
+    PN2_TUNING_KEYS(PN2_TUNING_LOAD)
+#undef PN2_TUNING_LOAD
+    return t;
+}
+
+Tuning tuning() { return t_depth > 0 ? t_tuning : shared_snapshot(); }
+
+// ---- device error slots
+static thread_local unsigned *t_slots[kMaxDevices] = {};
+static std::mutex g_default_read;
+
+static int current_device(int *dev) {
+    const hipError_t e = hipGetDevice(dev);
+    if (e != hipSuccess) return set_error(PN2_EHIP, "hipGetDevice: %s", hipGetErrorString(e));
+    if (*dev < 0 || *dev >= kMaxDevices) return set_error(PN2_EUNSUPPORTED, "device %d >= %d", *dev, kMaxDevices);
+    return PN2_OK;
+}
+
+unsigned *error_word() {
+    int d = 0;
+    if (hipGetDevice(&d) == hipSuccess && d >= 0 && d < kMaxDevices && t_slots[d]) return t_slots[d];
+    return default_error_slot();
+}
+
+// take (and with clear, reset) `slot`, stream-ordered on st, then wait for st
+static int take(unsigned *slot, int clear, uint32_t *bits, hipStream_t st, bool sync_device) {
+    unsigned v = 0;
+    hipError_t e = hipSuccess;
+    const char *what = "";
+    auto run = [&]() -> bool {
+        // every stream's work first (pn2_device_errors): kernels still in flight on other
+        // streams may raise bits
+        if (sync_device && (e = hipDeviceSynchronize()) != hipSuccess) { what = "hipDeviceSynchronize"; return false; }
+        if ((e = take_errors(slot, clear, &v, st)) != hipSuccess) { what = "take"; return false; }
+        return true;
+    };
+    bool ok;
+    if (slot == default_error_slot()) {  // shared with other threads: one reader at a time
+        std::lock_guard<std::mutex> g(g_default_read);
+        ok = run();
+    } else {
+        ok = run();
+    }
+    if (!ok) return set_error(PN2_EHIP, "pn2 device errors (%s): %s", what, hipGetErrorString(e));
+    *bits = v;
+    return PN2_OK;
+}
 }  // namespace pn2
 
 extern "C" int pn2_tuning_local(int enter) {
     if (enter) {
-        if (pn2::t_depth++ == 0) pn2::t_tuning = pn2::g_tuning;
+        if (pn2::t_depth++ == 0) pn2::t_tuning = pn2::shared_snapshot();
         return PN2_OK;
     }
     PN2_REQUIRE(pn2::t_depth > 0, "pn2_tuning_local: leave without enter");
@@ -39,21 +104,32 @@ extern "C" int pn2_tuning_local(int enter) {
 extern "C" const char *pn2_last_error(void) { return pn2::g_msg; }
 extern "C" int pn2_abi_version(void) { return PN2_ABI_VERSION; }
 
+extern "C" int pn2_error_slot_set(uint32_t *slot) {
+    int d = 0;
+    if (const int rc = pn2::current_device(&d)) return rc;
+    pn2::t_slots[d] = slot;
+    return PN2_OK;
+}
+
+extern "C" int pn2_error_slot_take(int clear, uint32_t *bits, void *stream) {
+    PN2_REQUIRE(bits, "pn2_error_slot_take: null pointer");
+    if (!pn2::default_error_slot()) return pn2::set_error(PN2_EHIP, "pn2_error_slot_take: no default slot");
+    return pn2::take(pn2::error_word(), clear, bits, pn2::as_stream(stream), false);
+}
+
 extern "C" int pn2_device_errors(int clear, uint32_t *bits) {
     PN2_REQUIRE(bits, "pn2_device_errors: null pointer");
-    unsigned a = 0, b = 0;
-    if (pn2::read_bq_errors(&a, clear) != 0 || pn2::read_group_errors(&b, clear) != 0)
-        return pn2::set_error(PN2_EHIP, "pn2_device_errors: %s", hipGetErrorString(hipGetLastError()));
-    *bits = a | b;
-    return PN2_OK;
+    if (!pn2::default_error_slot()) return pn2::set_error(PN2_EHIP, "pn2_device_errors: no default slot");
+    return pn2::take(pn2::error_word(), clear, bits, nullptr, true);
 }
 
 extern "C" int pn2_tuning_get(const char *key, int64_t *value) {
     PN2_REQUIRE(key && value, "pn2_tuning_get: null pointer");
-#define PN2_TUNING_GET(name, dflt)                 \
-    if (strcmp(key, #name) == 0) {                 \
-        *value = pn2::active().name;               \
-        return PN2_OK;                             \
+#define PN2_TUNING_GET(name, dflt)                                                           \
+    if (strcmp(key, #name) == 0) {                                                           \
+        *value = pn2::t_depth > 0 ? pn2::t_tuning.name                                       \
+                                  : pn2::g_tuning.name.load(std::memory_order_relaxed);      \
+        return PN2_OK;                                                                       \
     }
     PN2_TUNING_KEYS(PN2_TUNING_GET)
 #undef PN2_TUNING_GET
@@ -62,14 +138,27 @@ extern "C" int pn2_tuning_get(const char *key, int64_t *value) {
 
 extern "C" int pn2_tuning_set(const char *key, int64_t value) {
     PN2_REQUIRE(key, "pn2_tuning_set: null pointer");
-#define PN2_TUNING_SET(name, dflt)                 \
-    if (strcmp(key, #name) == 0) {                 \
-        pn2::active().name = value;                \
-        return PN2_OK;                             \
+#define PN2_TUNING_SET(name, dflt)                                                           \
+    if (strcmp(key, #name) == 0) {                                                           \
+        if (pn2::t_depth > 0) pn2::t_tuning.name = value;                                    \
+        else pn2::g_tuning.name.store(value, std::memory_order_relaxed);                     \
+        return PN2_OK;                                                                       \
     }
     PN2_TUNING_KEYS(PN2_TUNING_SET)
 #undef PN2_TUNING_SET
     return pn2::set_error(PN2_EINVAL, "pn2_tuning_set: unknown key '%s'", key);
+}
+
+extern "C" int pn2_tuning_default(const char *key, int64_t *value) {
+    PN2_REQUIRE(key && value, "pn2_tuning_default: null pointer");
+#define PN2_TUNING_DFLT(name, dflt)                \
+    if (strcmp(key, #name) == 0) {                 \
+        *value = dflt;                             \
+        return PN2_OK;                             \
+    }
+    PN2_TUNING_KEYS(PN2_TUNING_DFLT)
+#undef PN2_TUNING_DFLT
+    return pn2::set_error(PN2_EINVAL, "pn2_tuning_default: unknown key '%s'", key);
 }
 
 extern "C" const char *pn2_tuning_keys(void) {

@@ -348,446 +348,6 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
 #endif
 }
 
-// ------------------------------------------------------------------------- culled FPS (C = 3)
-// Diagnostic builds only (tools/debug/fps_cull_stats.py): -DPN2_FPS_STATS counts active chunks
-// per (wave, iteration); -DPN2_FPS_FLOOR skips every chunk after the first iteration (wrong
-// indices: the loop's fixed cost alone).
-#ifdef PN2_FPS_STAMPS
-// per (iteration < 128, wave < 16, point < 4) s_memtime of cloud 0: loop top, after the
-// activity test, after the chunk updates + wave candidate, after the barrier
-__device__ unsigned long long g_fps_stamps[128 * 16 * 4];
-extern "C" int pn2_debug_fps_stamps(unsigned long long *out) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fps_stamps), sizeof(g_fps_stamps)) == hipSuccess ? 0 : -1;
-}
-#define PN2_FPS_STAMP(k)                                                                        \
-    do {                                                                                       \
-        if (b == 0 && lane == 0 && it < 128)                                                   \
-            g_fps_stamps[(it * 16 + wave) * 4 + (k)] = __builtin_amdgcn_s_memtime();           \
-    } while (0)
-#else
-#define PN2_FPS_STAMP(k) do {} while (0)
-#endif
-#ifdef PN2_FPS_STATS
-__device__ unsigned long long g_fps_stats[4];
-extern "C" int pn2_debug_fps_stats(unsigned long long *out, int clear) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fps_stats), sizeof(g_fps_stats)) != hipSuccess) return -1;
-    if (clear) {
-        const unsigned long long z[4] = {0, 0, 0, 0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_fps_stats), z, sizeof(z)) != hipSuccess) return -1;
-    }
-    return 0;
-}
-#endif
-// The same serial loop with spatial ownership and exact culling.  In the prologue the cloud is
-// sorted into a Morton order of a coarse grid over its bounding box (a counting sort in LDS:
-// cell ranks by LDS atomics, a block scan, a scatter of the point indices); the sorted order is
-// cut into chunks of 64*PPC points, Q chunks per wave (chunk q of wave w is sorted chunk
-// q*NW + w), and lane l holds PPC points of each of its wave's chunks (registers, as above).  Each chunk is a compact region with a bounding box.
-//
-// Culling is exact.  For a centroid c and a box [lo, hi], q = clamp(c, lo, hi) is one of c, lo,
-// hi per channel, and LB = ((fl(qx-cx)^2 + fl(qy-cy)^2) + fl(qz-cz)^2) -- the reference's own
-// separately rounded ops -- is <= the distance the loop computes for every point of the box:
-// fl(p - c) is monotone in p and |p - c| >= |q - c| channel by channel, squares of magnitudes
-// and the rounded sums are monotone too.  So when LB >= the wave's current maximum of the
-// running distances, no point of the chunk can lower its distance (strict '<' update,
-// pointnet2_utils.py:64-66) and the chunk is skipped; a wave with no active chunk keeps its
-// candidate from the previous iteration.  Late in the run the new centroid's ball of influence
-// is small and most chunks of most waves skip.
-//
-// Ownership no longer follows the point index, so the tie rule (torch.max's first index among
-// the maxima, pointnet2_utils.py:67) is kept with explicit indices: per chunk the smallest
-// index among its points at the chunk maximum, per lane / wave the smallest among those at the
-// maximum, across waves the 64-bit key (dist bits : ~index) as before.
-template <int NT, int Q, int PPC, bool LDSC>
-__global__ __launch_bounds__(NT) void fps_cull_kernel(const float *__restrict__ pts, int N, int64_t sb,
-                                                      int64_t sn, int64_t sc,
-                                                      const int64_t *__restrict__ start, int S,
-                                                      int64_t *__restrict__ out_idx,
-                                                      float *__restrict__ out_pts,
-                                                      float *__restrict__ out_packed,
-                                                      float *__restrict__ pts_packed, int cp, int cbits) {
-    constexpr int NW = NT / 64, PPT = Q * PPC, CS = 64 * PPC;
-    static_assert(PPC % 2 == 0 && NW <= 16 && Q <= 32, "culled FPS shape");
-    __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b = blockIdx.x;
-    const float *P = pts + (int64_t)b * sb;
-    // a cloud's element offsets fit 32 bits (the host checks): 32-bit address math keeps the
-    // prologue's per-point loads out of scratch
-    const int isn = (int)sn, isc = (int)sc;
-    const int G3 = 1 << (3 * cbits);
-
-    // LDS: sidx [S] | key words (8) | slots [2][NW][8] (!LDSC) | cloud [N][4] (LDSC) |
-    //      cnt [G3] | perm [NT*PPT] | red [NW][8]
-    extern __shared__ __attribute__((aligned(16))) float fsm[];
-    int *sidx = reinterpret_cast<int *>(fsm);
-    const int hw = (S + 3) & ~3;
-    unsigned long long *key = reinterpret_cast<unsigned long long *>(fsm + hw);
-    float *slots = fsm + hw + 8;
-    float *cloud = slots + (LDSC ? 0 : 2 * NW * 8);
-    int *cnt = reinterpret_cast<int *>(cloud + (LDSC ? 4 * ((N + 3) & ~3) : 0));
-    int *perm = cnt + G3;
-    float *red = reinterpret_cast<float *>(perm + NT * PPT);
-
-    // ---- pass A: the points in index order, point n on thread n % NT (coalesced loads, one
-    // 16-byte packed record per lane per store), packed records, LDS cloud copy, bbox
-    for (int e = tid; e < G3; e += NT) cnt[e] = 0;
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int n = tid; n < N; n += NT) {
-        float pa[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            pa[k] = P[n * isn + k * isc];
-            lo[k] = fminf(lo[k], pa[k]);
-            hi[k] = fmaxf(hi[k], pa[k]);
-        }
-        if constexpr (LDSC) reinterpret_cast<float4 *>(cloud)[n] = float4{pa[0], pa[1], pa[2], 0.f};
-        if (pts_packed) {
-            // C = 3: every layout rule sums ((x^2 + y^2) + z^2)
-            const float4 r4 = {pa[0], pa[1], pa[2],
-                               __fadd_rn(__fadd_rn(__fmul_rn(pa[0], pa[0]), __fmul_rn(pa[1], pa[1])),
-                                         __fmul_rn(pa[2], pa[2]))};
-            *reinterpret_cast<float4 *>(pts_packed + ((int64_t)b * N + n) * 4) = r4;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        for (int o = 32; o >= 1; o >>= 1) {
-            lo[k] = fminf(lo[k], __shfl_xor(lo[k], o));
-            hi[k] = fmaxf(hi[k], __shfl_xor(hi[k], o));
-        }
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            red[wave * 8 + k] = lo[k];
-            red[wave * 8 + 3 + k] = hi[k];
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        lo[k] = red[k];
-        hi[k] = red[3 + k];
-        for (int w = 1; w < NW; ++w) {
-            lo[k] = fminf(lo[k], red[w * 8 + k]);
-            hi[k] = fmaxf(hi[k], red[w * 8 + 3 + k]);
-        }
-    }
-    // ---- pass B: Morton cell of every point (any mapping is exact; this one makes chunks
-    // compact) and its rank within the cell: cell << 16 | rank
-    const int g = 1 << cbits;
-    float scl[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float ext = hi[k] - lo[k];
-        scl[k] = ext > 0.f ? (float)g / ext : 0.f;
-    }
-    int pr[PPT];
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int n = tid * PPT + j;
-        unsigned code = 0;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const float x = n < N ? (LDSC ? cloud[4 * n + k] : P[n * isn + k * isc]) : 0.f;
-            const float v = (x - lo[k]) * scl[k];
-            unsigned ci = (v >= 0.f && v < (float)g) ? (unsigned)v : (v >= (float)g ? (unsigned)(g - 1) : 0u);  // NaN -> 0
-            // spread the (<= 4) bits of ci to every third bit
-            ci = (ci | (ci << 4)) & 0x0C3u;
-            ci = (ci | (ci << 2)) & 0x249u;
-            code |= ci << k;
-        }
-        pr[j] = n < N ? (int)(code << 16) | atomicAdd(&cnt[code], 1) : 0;
-    }
-    __syncthreads();
-    // ---- exclusive scan of the cell counts (each thread E consecutive cells)
-    {
-        const int E = (G3 + NT - 1) / NT;
-        const int e0 = tid * E;
-        int sum = 0;
-        for (int e = 0; e < E; ++e)
-            if (e0 + e < G3) sum += cnt[e0 + e];
-        int inc = sum;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(inc, o);
-            if (lane >= o) inc += v;
-        }
-        if (lane == 63) reinterpret_cast<int *>(red)[wave * 8 + 6] = inc;  // red[..6] is not the bbox
-        __syncthreads();
-        int base = inc - sum;
-        for (int w = 0; w < wave; ++w) base += reinterpret_cast<int *>(red)[w * 8 + 6];
-        for (int e = 0; e < E; ++e)
-            if (e0 + e < G3) {
-                const int c = cnt[e0 + e];
-                cnt[e0 + e] = base;
-                base += c;
-            }
-    }
-    __syncthreads();
-    // ---- pass C: scatter the point indices into sorted order
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) {
-        const int n = tid * PPT + j;
-        if (n < N) perm[cnt[pr[j] >> 16] + (pr[j] & 0xFFFF)] = n;
-    }
-    __syncthreads();
-
-    // ---- pass D: this lane's points: chunk q of wave w = sorted positions (qNW + w) * CS ..,
-    // lane l takes PPC consecutive ones (their indices stay in LDS: perm).  Per channel one
-    // register vector, so a wave-uniform register index picks a point's coordinates.
-    typedef float VQ __attribute__((ext_vector_type(PPT)));
-    VQ X[3];
-    unsigned dist[PPT];
-    // chunk q of wave w is sorted chunk q * NW + w: neighbouring chunks (in Morton order) sit
-    // in different waves, so the few chunks near a new centroid are updated in parallel on
-    // several SIMDs rather than one after another by one wave
-    const int *myperm = perm + wave * CS + lane * PPC;  // + q * NW * CS + i
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-#pragma unroll
-        for (int i = 0; i < PPC; ++i) {
-            const int j = q * PPC + i;
-            const int s = (q * NW + wave) * CS + lane * PPC + i;
-            const int n = s < N ? myperm[q * NW * CS + i] : -1;
-            dist[j] = n >= 0 ? __float_as_uint(1e10f) : 0u;  // padding: 0, never the maximum's first index
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                float v = 0.f;
-                if (n >= 0) v = LDSC ? cloud[4 * n + k] : P[n * isn + k * isc];
-                X[k][j] = v;
-            }
-        }
-    }
-    // padding positions read as index 0x7FFFFFFF (after every real point)
-    for (int s = N + tid; s < NT * PPT; s += NT) perm[s] = 0x7FFFFFFF;
-    // chunk boxes: lane q of the wave holds chunk q's box (empty chunk: lo = +inf, hi = -inf,
-    // whose LB is +inf or NaN -- never active, and it holds no point that could change)
-    float blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            float l = INFINITY, h = -INFINITY;
-#pragma unroll
-            for (int i = 0; i < PPC; ++i)
-                if (dist[q * PPC + i] != 0u) {
-                    l = fminf(l, X[k][q * PPC + i]);
-                    h = fmaxf(h, X[k][q * PPC + i]);
-                }
-            for (int o = 32; o >= 1; o >>= 1) {
-                l = fminf(l, __shfl_xor(l, o));
-                h = fmaxf(h, __shfl_xor(h, o));
-            }
-            if (lane == q) {
-                blo[k] = l;
-                bhi[k] = h;
-            }
-        }
-    }
-    __syncthreads();  // the padding indices are in perm
-    // per chunk: the lane's maximum of the running distances, the smallest index at it and
-    // that point's place in the chunk
-    unsigned cm[Q], cb[Q];
-    int ci[Q];
-    // point indices of the lane's chunks: registers for small PPT, else read from perm (LDS)
-    // at the start of an active chunk's update, before its distance math
-    constexpr bool IDXREG = PPT <= 8;
-    unsigned preg[IDXREG ? PPT : 1];
-    if constexpr (IDXREG) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-#pragma unroll
-            for (int i = 0; i < PPC; ++i) preg[q * PPC + i] = (unsigned)myperm[q * NW * CS + i];
-    }
-    auto chunk_idx = [&](int q, unsigned (&pi)[PPC]) {
-        if constexpr (IDXREG) {
-#pragma unroll
-            for (int i = 0; i < PPC; ++i) pi[i] = preg[q * PPC + i];
-        } else if constexpr (PPC == 4) {
-            const int4 v = *reinterpret_cast<const int4 *>(myperm + q * NW * CS);
-            pi[0] = v.x; pi[1] = v.y; pi[2] = v.z; pi[3] = v.w;
-        } else if constexpr (PPC == 2) {
-            const int2 v = *reinterpret_cast<const int2 *>(myperm + q * NW * CS);
-            pi[0] = v.x; pi[1] = v.y;
-        } else {
-#pragma unroll
-            for (int i = 0; i < PPC; ++i) pi[i] = (unsigned)myperm[q * NW * CS + i];
-        }
-    };
-    auto chunk_best = [&](int q, const unsigned (&pi)[PPC]) {
-        unsigned m = dist[q * PPC];
-#pragma unroll
-        for (int i = 1; i < PPC; ++i) m = max(m, dist[q * PPC + i]);
-        unsigned bi = 0xFFFFFFFFu;
-        int bii = 0;
-#pragma unroll
-        for (int i = 0; i < PPC; ++i)
-            if (dist[q * PPC + i] == m && pi[i] < bi) {
-                bi = pi[i];
-                bii = i;
-            }
-        cm[q] = m;
-        cb[q] = bi;
-        ci[q] = bii;
-    };
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        unsigned pi[PPC];
-        chunk_idx(q, pi);
-        chunk_best(q, pi);
-    }
-
-    // the wave's candidate: its maximum, the smallest index at it, and (!LDSC) its coordinates
-    unsigned wv = 0, wi = 0x7FFFFFFFu;
-    float wc[3] = {0.f, 0.f, 0.f};
-    auto wave_best = [&]() {
-        unsigned bv = cm[0];
-#pragma unroll
-        for (int q = 1; q < Q; ++q) bv = max(bv, cm[q]);
-        unsigned bi = 0xFFFFFFFFu;
-        int bj = 0;
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-            if (cm[q] == bv && cb[q] < bi) {
-                bi = cb[q];
-                bj = q * PPC + ci[q];
-            }
-        wv = wave_max_u32(bv);
-        const unsigned long long tie = __ballot(bv == wv);
-        int ol = (int)__builtin_ctzll(tie);
-        if (__builtin_popcountll(tie) == 1) {
-            wi = (unsigned)__builtin_amdgcn_readlane((int)bi, ol);
-        } else {
-            wi = wave_min_u32(bv == wv ? bi : 0xFFFFFFFFu);
-            ol = (int)__builtin_ctzll(__ballot(bv == wv && bi == wi));
-        }
-        if constexpr (!LDSC) {  // the owner lane's register of point wi: one indexed move per channel
-            const int j = __builtin_amdgcn_readlane(bj, ol);
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-                wc[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(X[k][j]), ol));
-        }
-    };
-    wave_best();
-
-    int far = (int)start[b];
-    float c[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) c[k] = P[far * isn + k * isc];
-    if (tid < 3) key[tid] = 0ull;
-    __syncthreads();
-
-    for (int it = 0;; ++it) {
-        if (tid == 0) sidx[it] = far;
-        if (it == S - 1) break;
-        PN2_FPS_STAMP(0);
-        // lane q < Q tests chunk q against the wave's maximum
-        float lb;
-        {
-            float s3[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const float d = fminf(fmaxf(c[k], blo[k]), bhi[k]) - c[k];
-                s3[k] = d * d;
-            }
-            lb = (s3[0] + s3[1]) + s3[2];
-        }
-        unsigned act = (unsigned)__ballot(lane < Q && !(__float_as_uint(lb) >= wv));
-#ifdef PN2_FPS_FLOOR
-        if (it > 0) act = 0u;
-#endif
-        PN2_FPS_STAMP(1);
-#ifdef PN2_FPS_STATS
-        if (lane == 0) {
-            atomicAdd(&g_fps_stats[0], (unsigned long long)__builtin_popcount(act));
-            atomicAdd(&g_fps_stats[1], (unsigned long long)Q);
-            atomicAdd(&g_fps_stats[2], act ? 1ull : 0ull);
-            atomicAdd(&g_fps_stats[3], 1ull);
-        }
-#endif
-        if (act != 0u) {
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                if (act & (1u << q)) {
-                    unsigned pi[PPC];
-                    chunk_idx(q, pi);  // (LDS: in flight during the distance math)
-#pragma unroll
-                    for (int h = 0; h < PPC / 2; ++h) {
-                        const int j = q * PPC + 2 * h;
-                        pn2_f2 s3[3];
-#pragma unroll
-                        for (int k = 0; k < 3; ++k) {
-                            const pn2_f2 d = pn2_f2{X[k][j], X[k][j + 1]} - c[k];
-                            s3[k] = d * d;
-                        }
-                        const pn2_f2 dd = (s3[0] + s3[1]) + s3[2];
-                        dist[j] = min(dist[j], __float_as_uint(dd.x));
-                        dist[j + 1] = min(dist[j + 1], __float_as_uint(dd.y));
-                    }
-                    chunk_best(q, pi);
-                }
-            }
-            wave_best();
-        }
-        PN2_FPS_STAMP(2);
-        if constexpr (LDSC) {
-            if (lane == 0) atomicMax(&key[it % 3], ((unsigned long long)wv << 32) | (0xFFFFFFFFu - wi));
-            if (tid == 64) key[(it + 1) % 3] = 0ull;
-            __syncthreads();
-            far = __builtin_amdgcn_readfirstlane((int)(0xFFFFFFFFu - (unsigned)key[it % 3]));
-            const float4 r4 = reinterpret_cast<const float4 *>(cloud)[far];
-            c[0] = r4.x;
-            c[1] = r4.y;
-            c[2] = r4.z;
-        } else {
-            // the same 64-bit key max; each wave's candidate coordinates (and index) sit in its
-            // slot (double-buffered by parity), read by lanes 0..NW-1 beside the key
-            const int par = it & 1;
-            if (lane == 0) {
-                atomicMax(&key[it % 3], ((unsigned long long)wv << 32) | (0xFFFFFFFFu - wi));
-                reinterpret_cast<float4 *>(slots)[par * NW + wave] = float4{wc[0], wc[1], wc[2], __uint_as_float(wi)};
-            }
-            if (tid == 64) key[(it + 1) % 3] = 0ull;
-            __syncthreads();
-            PN2_FPS_STAMP(3);
-            const unsigned kw = (unsigned)key[it % 3];
-            float4 sv = {0.f, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)};
-            if (lane < NW) sv = reinterpret_cast<const float4 *>(slots)[par * NW + lane];
-            far = __builtin_amdgcn_readfirstlane((int)(0xFFFFFFFFu - kw));
-            const int gw = (int)__builtin_ctzll(__ballot(lane < NW && __float_as_uint(sv.w) == (unsigned)far));
-            c[0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv.x), gw));
-            c[1] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv.y), gw));
-            c[2] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv.z), gw));
-        }
-    }
-    __syncthreads();
-
-    // ---- outputs: indices, gathered centroids (index_points), packed centroids
-    for (int i = tid; i < S; i += NT) {
-        const int n = sidx[i];
-        out_idx[(int64_t)b * S + i] = n;
-        if (out_pts || out_packed) {
-            float q3[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) q3[k] = P[n * isn + k * isc];
-            if (out_pts) {
-                float *o = out_pts + ((int64_t)b * S + i) * 3;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) o[k] = q3[k];
-            }
-            if (out_packed) {
-                float *o = out_packed + ((int64_t)b * S + i) * cp;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) o[k] = q3[k];
-                o[3] = __fadd_rn(__fadd_rn(__fmul_rn(q3[0], q3[0]), __fmul_rn(q3[1], q3[1])), __fmul_rn(q3[2], q3[2]));
-            }
-        }
-    }
-}
-
 // ------------------------------------------------------------------------- streamed FPS
 // Any N and S: nothing of the cloud is register-resident.  Each iteration every thread walks
 // the points n = tid, tid + NT, ... (coalesced reads of the input for either layout), computes
@@ -1013,71 +573,6 @@ static int dispatch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64
     return set_error(PN2_EUNSUPPORTED, "pn2_fps_f32: N=%lld: no register-resident shape", (long long)N);
 }
 
-// culled FPS (C = 3): LDS bytes with / without the cloud copy, the grid's cell bits
-static int fps_cull_bits(int64_t N) {
-    int l = 0;  // about 4 points per cell: 3 * bits = floor(log2(N / 4))
-    while (((int64_t)4 << (l + 1)) <= N) ++l;
-    const int bits = l / 3;
-    return bits < 1 ? 1 : (bits > 4 ? 4 : bits);
-}
-static size_t fps_cull_lds(int64_t N, int64_t S, int NT, int PPT, bool ldsc) {
-    const int NW = NT / 64;
-    size_t sz = (size_t)((S + 3) & ~3) * 4 + 32;
-    sz += ldsc ? (size_t)((N + 3) & ~3) * 16 : (size_t)2 * NW * 32;
-    sz += (size_t)4 << (3 * fps_cull_bits(N));
-    sz += (size_t)NT * PPT * 4 + (size_t)NW * 32;
-    return sz;
-}
-
-template <int NT, int Q, int PPC>
-static int launch_fps_cull(const float *pts, int64_t B, int64_t N, int64_t sb, int64_t sn, int64_t sc,
-                           const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
-                           float *out_packed, float *pts_packed, hipStream_t st) {
-    constexpr int PPT = Q * PPC;
-    const bool ldsc = (size_t)N * 16 <= (size_t)kFpsLdsCloud && fps_cull_lds(N, S, NT, PPT, true) <= (size_t)160 * 1024;
-    const size_t lds = fps_cull_lds(N, S, NT, PPT, ldsc);
-    PN2_REQUIRE(lds <= (size_t)160 * 1024, "pn2_fps_f32: culled FPS LDS %zu", lds);
-    const int bits = fps_cull_bits(N);
-#define PN2_FPS_CULL_L(LD)                                                                                  \
-    do {                                                                                                    \
-        static const hipError_t attr = hipFuncSetAttribute(                                                \
-            reinterpret_cast<const void *>(&fps_cull_kernel<NT, Q, PPC, LD>),                              \
-            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                                       \
-        PN2_REQUIRE(attr == hipSuccess, "pn2_fps_f32: LDS attribute");                                     \
-        hipLaunchKernelGGL((fps_cull_kernel<NT, Q, PPC, LD>), dim3((unsigned)B), dim3(NT), lds, st, pts,   \
-                           (int)N, sb, sn, sc, start, (int)S, out_idx, out_pts, out_packed, pts_packed,    \
-                           (int)pn2_packed_stride(3), bits);                                               \
-    } while (0)
-    if (ldsc) PN2_FPS_CULL_L(true);
-    else PN2_FPS_CULL_L(false);
-#undef PN2_FPS_CULL_L
-    PN2_LAUNCH_CHECK("fps_cull_kernel");
-    return PN2_OK;
-}
-
-// the culled kernel's block shapes (xyz clouds of 257..16384 points); tuning fps_cull = 0
-// keeps the index-ordered kernel, fps_cull = NT*100 + Q*10 + PPC forces a compiled shape
-static int dispatch_fps_cull(const float *pts, int64_t B, int64_t N, int64_t sb, int64_t sn, int64_t sc,
-                             const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
-                             float *out_packed, float *pts_packed, hipStream_t st) {
-#define A pts, B, N, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed, st
-    const int64_t f = tuning().fps_cull;
-#define PN2_CULL_TRY(nt, q, ppc) \
-    if (f == nt * 100 + q * 10 + ppc && N <= (int64_t)nt * q * ppc) return launch_fps_cull<nt, q, ppc>(A);
-    PN2_CULL_TRY(256, 1, 2) PN2_CULL_TRY(256, 1, 4) PN2_CULL_TRY(256, 2, 2) PN2_CULL_TRY(512, 1, 2)
-    PN2_CULL_TRY(1024, 1, 2) PN2_CULL_TRY(1024, 2, 2) PN2_CULL_TRY(1024, 1, 4) PN2_CULL_TRY(1024, 2, 4)
-    PN2_CULL_TRY(1024, 4, 2) PN2_CULL_TRY(1024, 4, 4) PN2_CULL_TRY(1024, 8, 2)
-    PN2_CULL_TRY(256, 8, 4) PN2_CULL_TRY(512, 8, 4) PN2_CULL_TRY(512, 16, 2) PN2_CULL_TRY(512, 4, 8)
-#undef PN2_CULL_TRY
-    if (N <= 512) return launch_fps_cull<256, 1, 2>(A);
-    if (N <= 1024) return launch_fps_cull<256, 2, 2>(A);
-    if (N <= 2048) return launch_fps_cull<1024, 1, 2>(A);
-    if (N <= 4096) return launch_fps_cull<1024, 2, 2>(A);
-    if (N <= 8192) return launch_fps_cull<1024, 4, 2>(A);
-    return launch_fps_cull<1024, 4, 4>(A);
-#undef A
-}
-
 // the register-resident kernels' limits (dispatch_fps); past them the streamed kernel
 static bool fps_resident(int64_t N, int64_t S) { return N <= 16384 && S <= kFpsMaxS; }
 static size_t fps_stream_lds(int64_t N) { return (size_t)2 * (kFpsStreamT / 64) * 8 + (size_t)N * 4; }
@@ -1133,10 +628,6 @@ extern "C" int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C,
         if (C == 10) return launch_fps_stream<10, true>(A, ws, st);
         return launch_fps_stream<kMaxC, false>(A, ws, st);
     }
-    // (the culled kernel addresses a cloud with 32-bit element offsets)
-    const bool off32 = sn >= 0 && sc >= 0 && (N - 1) * sn + 2 * sc < (int64_t)INT32_MAX;
-    if (C == 3 && N > 256 && off32 && tuning().fps_cull != 0 && tuning().fps_threads == 0)
-        return dispatch_fps_cull(pts, B, N, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed, st);
     if (C == 3) return dispatch_fps<3, true, 16384>(A, st);
     if (C == 10) return dispatch_fps<10, true, 8192>(A, st);
     return dispatch_fps<kMaxC, false, 4096>(A, st);

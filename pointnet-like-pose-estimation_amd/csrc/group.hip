@@ -10,53 +10,70 @@
 //
 // Indices follow torch's advanced indexing: -N <= n < 0 counts from the end.  Outside [-N, N)
 // the reference raises IndexError; a kernel cannot, so the element is NaN (never an
-// out-of-bounds read) and PN2_DEVERR_INDEX is raised in the device error word
-// (pn2_device_errors; pn2.check_device_errors() raises IndexError).
+// out-of-bounds read) and PN2_DEVERR_INDEX is raised in the launching thread's device error slot
+// (pn2_error_slot_set / pn2_device_errors; pn2.check_device_errors() raises IndexError).
+#include <atomic>
+
 #include "pn2_internal.h"
 
 namespace pn2 {
 
-__device__ unsigned g_group_errors;
+// the process-wide default error slot (pn2_internal.h): [0] bits, [1] the take's snapshot
+__device__ unsigned g_default_errors[2];
 
-// torch's index rule; -1 when out of range (and the error word raised)
-__device__ __forceinline__ int64_t torch_index(int64_t n, int64_t N) {
+unsigned *default_error_slot() {
+    static std::atomic<unsigned *> cache[kMaxDevices];
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDevices) return nullptr;
+    unsigned *p = cache[d].load(std::memory_order_acquire);
+    if (!p) {
+        void *a = nullptr;
+        if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_default_errors)) != hipSuccess) return nullptr;
+        p = static_cast<unsigned *>(a);
+        cache[d].store(p, std::memory_order_release);
+    }
+    return p;
+}
+
+// the slot's value (and, with clear, its reset) in ONE device atomic: a bit that a kernel ORs in
+// between cannot be lost (a read followed by a separate clear could drop it)
+__global__ void errors_take_kernel(unsigned *slot, int clear) {
+    slot[1] = clear ? atomicExch(&slot[0], 0u) : atomicOr(&slot[0], 0u);
+}
+
+hipError_t take_errors(unsigned *slot, int clear, unsigned *bits, hipStream_t st) {
+    hipLaunchKernelGGL(errors_take_kernel, dim3(1), dim3(1), 0, st, slot, clear);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    unsigned v = 0;
+    if ((e = hipMemcpyAsync(&v, slot + 1, sizeof(v), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    *bits = v;
+    return hipSuccess;
+}
+
+// torch's index rule; -1 when out of range (and the error bit raised in the launch's slot)
+__device__ __forceinline__ int64_t torch_index(int64_t n, int64_t N, unsigned *err) {
     if (n < 0) n += N;
     if (n < 0 || n >= N) {
-        atomicOr(&g_group_errors, (unsigned)PN2_DEVERR_INDEX);
+        atomicOr(err, (unsigned)PN2_DEVERR_INDEX);
         return -1;
     }
     return n;
-}
-
-// the word's value (and, with clear, its reset) in ONE device atomic: a bit that a kernel ORs in
-// between cannot be lost (a read followed by a separate clear could drop it)
-__device__ unsigned g_group_snapshot;
-__global__ void group_errors_take_kernel(int clear) {
-    g_group_snapshot = clear ? atomicExch(&g_group_errors, 0u) : atomicOr(&g_group_errors, 0u);
-}
-
-int read_group_errors(unsigned *bits, int clear) {
-    // every stream's work first: kernels still in flight on other streams may raise bits
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    hipLaunchKernelGGL(group_errors_take_kernel, dim3(1), dim3(1), 0, 0, clear);
-    if (hipGetLastError() != hipSuccess) return -1;
-    unsigned v = 0;
-    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_group_snapshot), sizeof(v)) != hipSuccess) return -1;
-    *bits = v;
-    return 0;
 }
 
 __global__ __launch_bounds__(256) void index_points_kernel(const float *__restrict__ pts,
                                                            int64_t B, int64_t N, int64_t C,
                                                            int64_t sb, int64_t sn, int64_t sc,
                                                            const int64_t *__restrict__ idx,
-                                                           int64_t M, float *__restrict__ out) {
+                                                           int64_t M, float *__restrict__ out,
+                                                           unsigned *err) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= B * M * C) return;
     const int64_t c = e % C;
     const int64_t bm = e / C;
     const int64_t b = bm / M;
-    const int64_t n = torch_index(idx[bm], N);
+    const int64_t n = torch_index(idx[bm], N, err);
     out[e] = n < 0 ? __builtin_nanf("") : pts[b * sb + n * sn + c * sc];
 }
 
@@ -67,7 +84,7 @@ __global__ __launch_bounds__(256) void group_kernel(const float *__restrict__ pt
                                                     const float *__restrict__ ctr, int64_t S,
                                                     const int64_t *__restrict__ idx, int64_t K,
                                                     int feature_first, int64_t total,
-                                                    float *__restrict__ out) {
+                                                    float *__restrict__ out, unsigned *err) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= total) return;
     const int64_t W = C + D;
@@ -75,7 +92,7 @@ __global__ __launch_bounds__(256) void group_kernel(const float *__restrict__ pt
     const int64_t row = e / W;  // (b*S + s)*K + k
     const int64_t g = row / K;
     const int64_t b = g / S;
-    const int64_t n = torch_index(idx[row], N);
+    const int64_t n = torch_index(idx[row], N, err);
     const int64_t xc = feature_first ? ch - D : ch;  // xyz channel, if any
     float v;
     if (n < 0)
@@ -100,8 +117,10 @@ extern "C" int pn2_index_points_f32(const float *pts, int64_t B, int64_t N, int6
     PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && M >= 0, "pn2_index_points_f32: bad shape");
     const int64_t tot = B * M * C;
     if (tot == 0) return PN2_OK;
+    unsigned *err = error_word();
+    PN2_REQUIRE(err, "pn2_index_points_f32: no device error slot");
     hipLaunchKernelGGL(index_points_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                       as_stream(stream), pts, B, N, C, sb, sn, sc, idx, M, out);
+                       as_stream(stream), pts, B, N, C, sb, sn, sc, idx, M, out, err);
     PN2_LAUNCH_CHECK("index_points_kernel");
     return PN2_OK;
 }
@@ -117,9 +136,11 @@ extern "C" int pn2_group_f32(const float *pts, int64_t B, int64_t N, int64_t C, 
                 "pn2_group_f32: bad shape");
     const int64_t tot = B * S * K * (C + D);
     if (tot == 0) return PN2_OK;
+    unsigned *err = error_word();
+    PN2_REQUIRE(err, "pn2_group_f32: no device error slot");
     hipLaunchKernelGGL(group_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
                        as_stream(stream), pts, N, C, sb, sn, sc, feat, D, fb, fn, fd, ctr, S, idx,
-                       K, feature_first, tot, out);
+                       K, feature_first, tot, out, err);
     PN2_LAUNCH_CHECK("group_kernel");
     return PN2_OK;
 }

@@ -17,9 +17,11 @@ int set_error(int code, const char *fmt, ...);
         if (!(cond)) return ::pn2::set_error(PN2_EINVAL, __VA_ARGS__); \
     } while (0)
 
+// the launch's own error (hipGetLastError returns, and resets, the first error since the last
+// call; its value is the one reported -- not a second call's hipSuccess)
 #define PN2_LAUNCH_CHECK(what)                                                        \
     do {                                                                              \
-        hipError_t e_ = hipGetLastError();                                            \
+        const hipError_t e_ = hipGetLastError();                                      \
         if (e_ != hipSuccess)                                                         \
             return ::pn2::set_error(PN2_EHIP, "%s: %s", what, hipGetErrorString(e_)); \
     } while (0)
@@ -27,7 +29,8 @@ int set_error(int code, const char *fmt, ...);
 static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ------------------------------------------------------------------ kernel-selection tuning
-// Process-wide parameters of the launch choices (defaults = the measured best).  Nothing reads
+// Parameters of the launch choices (defaults = the measured best): process-wide (one atomic word
+// per key, errors.cpp) or a thread's own copy (pn2_tuning_local).  Nothing reads
 // the environment: tests and A/B tools set them through pn2_tuning_set (pn2/tuning.py parses
 // the one PN2_TUNING variable).  X(name, default)
 #define PN2_TUNING_KEYS(X)                                                                     \
@@ -45,8 +48,6 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(fps_mid, 512)        /* automatic FPS block for 256 < N <= 1024: 512 threads x 2      */ \
                            /* points (fastest alone: the eager forward) or 256 x 4 (the     */ \
                            /* pipelines' geometry, beside the chains)                       */ \
-    X(fps_cull, 0)         /* 1: culled FPS for xyz clouds (0: the index-ordered kernel)    */ \
-                           /* (NT*100 + Q*10 + PPC: force a compiled culled shape)          */ \
     X(dense_maxntc, 2)     /* widest 32-column tile count of the 4-wave dense layer         */ \
     X(dense_minwg, 256)    /* workgroups a wider dense tile must still leave                 */ \
     X(dense_wide_minwg, 512) /* workgroups the 256 x 128 dense tile must leave              */ \
@@ -63,12 +64,18 @@ struct Tuning {
     PN2_TUNING_KEYS(PN2_TUNING_FIELD)
 #undef PN2_TUNING_FIELD
 };
-const Tuning &tuning();
+// a snapshot of the calling thread's keys (its pn2_tuning_local copy, else the process-wide ones)
+Tuning tuning();
 
-// device error words (pn2_device_errors): each translation unit that can raise one keeps its
-// own __device__ word; these read (and optionally clear) it, synchronously
-int read_group_errors(unsigned *bits, int clear);
-int read_bq_errors(unsigned *bits, int clear);
+// ---- device error slots (pn2_error_slot_set): two device words, [0] the PN2_DEVERR_* bits the
+// kernels OR in, [1] the take kernel's snapshot.  error_word(): the launching thread's slot on
+// the current device, else the process-wide default slot (a __device__ array, group.hip).
+constexpr int kMaxDevices = 64;
+unsigned *error_word();
+unsigned *default_error_slot();  // the current device's default slot; nullptr on a HIP error
+// one device atomic takes slot[0] (and with clear resets it: a bit raised meanwhile is never
+// lost) into slot[1], copied to *bits; stream-ordered on st, which it then waits for
+hipError_t take_errors(unsigned *slot, int clear, unsigned *bits, hipStream_t st);
 
 constexpr int kMaxC = 16;  // point dims (xyz + one-hot) held in registers
 

@@ -139,15 +139,6 @@ __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const floa
         a4[m] = *reinterpret_cast<const cfloatx4 *>(al + 32 * t + 8 * m + 4 * h);
         b4[m] = *reinterpret_cast<const cfloatx4 *>(be + 32 * t + 8 * m + 4 * h);
     }
-#ifdef PN2_ABL_NOEPI
-    (void)a4; (void)b4;  // ablation (timing only): the accumulator bits as the next operand
-    lo.h = __builtin_bit_cast(bf16x8, cfloatx4{acc[0], acc[1], acc[2], acc[3]});
-    hi.h = __builtin_bit_cast(bf16x8, cfloatx4{acc[8], acc[9], acc[10], acc[11]});
-    lo.m = __builtin_bit_cast(bf16x8, cfloatx4{acc[4], acc[5], acc[6], acc[7]});
-    hi.m = __builtin_bit_cast(bf16x8, cfloatx4{acc[12], acc[13], acc[14], acc[15]});
-    lo.l = lo.h;
-    hi.l = hi.m;
-#else
     float y0[8], y1[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -156,7 +147,6 @@ __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const floa
     }
     lo = splitN<NP>(y0);
     hi = splitN<NP>(y1);
-#endif
 }
 
 
@@ -196,15 +186,7 @@ template <int NP>
 __device__ __forceinline__ Split hid_split(const Split &x) { return x; }
 template <int NP>
 __device__ __forceinline__ Split hid_split(const F8 &x) {
-#ifdef PN2_ABL_NOEPI
-    Split r;  // ablation (timing only)
-    r.h = __builtin_bit_cast(bf16x8, cfloatx4{x.v[0], x.v[1], x.v[2], x.v[3]});
-    r.m = __builtin_bit_cast(bf16x8, cfloatx4{x.v[4], x.v[5], x.v[6], x.v[7]});
-    r.l = r.h;
-    return r;
-#else
     return splitN<NP>(x.v);
-#endif
 }
 __device__ __forceinline__ unsigned hid_dep(const Split &x) {
     return __builtin_bit_cast(unsigned, __builtin_shufflevector(x.h, x.h, 0, 1));
@@ -355,9 +337,6 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     };
     const int n0 = T0 * L0.kb;
     auto issue_stage = [&](int st) {  // this wave's step of stage st
-#ifdef PN2_ABL_NODMA
-        if (st >= 0) return;  // ablation (timing only): the ring is never filled
-#endif
         const int x = st * kChainWaves + wave;
         char *dst = ring + (st % KS) * kStageBytes + wave * kStepBytes;
         if constexpr (KB0M > 0) {
@@ -414,22 +393,16 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     const unsigned ring3 = (unsigned)(size_t)(__attribute__((address_space(3))) char *)ring;
     auto rd = [&](Split &w) {
         if ((nr & (kChainWaves - 1)) == 0) {  // first step of a stage: see read_w
-#ifndef PN2_ABL_NOBAR
             ring_fence();
             stage_wait<NP, KS>();
             stage_barrier();
-#endif
             issue_stage(nr / kChainWaves + KS - 1);
         }
         const unsigned a = ring3 + (unsigned)(((nr / kChainWaves) % KS) * kStageBytes +
                                               (nr & (kChainWaves - 1)) * kStepBytes) + loff;
-#ifdef PN2_ABL_NOLDS
-        asm volatile("" : "+v"(w.h), "+v"(w.m), "+v"(w.l) : "v"(a));  // ablation (timing only)
-#else
         asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:1024\n\tds_read_b128 %2, %3 offset:2048"
                      : "=&v"(w.h), "=&v"(w.m), "=&v"(w.l)
                      : "v"(a));
-#endif
         ++nr;
     };
     auto wt3 = [&](Split &w) { asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(w.h), "+v"(w.m), "+v"(w.l)); };
@@ -455,11 +428,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         const int k = (urow_e >> 4) & 15, nv = (urow_e & 7) + 1;
         g = valid ? c_g0 + (unsigned)(urow_e >> 8) : c_g0;
         const int j = kUnitRows * k + ((r & 7) < nv ? (r & 7) : 0);
-#ifdef PN2_ABL_NOGATHER
-        n = (int)(g & 63u);  // ablation (timing only): no neighbour-index load
-#else
         n = valid ? src_index(s, (int64_t)g * A.K + j) : 0;
-#endif
     } else {
         const unsigned R = (unsigned)slab * 32u + (unsigned)r;
         valid = R < (unsigned)A.M;

@@ -205,16 +205,8 @@ void dense_split_kernel(const DenseSplitArgs A) {
     auto load_fast = [&](int c, float (&x)[kKC][8]) {
         const int kb0 = c * kKC;
         if (kb0 + kKC <= A.kb) {
-#ifdef PN2_DENSE_DIAG_COALESCED
-            // diagnostic only (wrong results): rows mode reads the same bytes per wave as
-            // whole lines
-            const float *p = A.mode == 0 ? A.rows + (int64_t)(row0 + 32 * wave) * A.rs + 16 * kb0 * 32 + lane * 4
-                                         : lrow + 16 * kb0;
-            const int ks = A.mode == 0 ? 512 : 16, rs_ = A.mode == 0 ? 256 : 8;
-#else
             const float *p = lrow + 16 * kb0;
             constexpr int ks = 16, rs_ = 8;
-#endif
 #pragma unroll
             for (int k = 0; k < kKC; ++k)
 #pragma unroll
@@ -641,16 +633,8 @@ void dense_lds_kernel(const DenseSplitArgs A) {
         }
     };
     auto mfma_kb = [&](const Split &xs, const Frags &f, int kbl) {
-#ifdef PN2_DENSE_DIAG_NOMFMA  // diagnostic builds only (wrong results): no MFMAs in the loop
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
-            asm volatile("" ::"v"(xs.h), "v"(xs.m), "v"(xs.l), "v"(f.b[kbl][i].h), "v"(f.b[kbl][i].m), "v"(f.b[kbl][i].l));
-            acc[i][0] += 1.f;
-        }
-#else
 #pragma unroll
         for (int i = 0; i < NT; ++i) acc[i] = mma_wb<NP>(xs, f.b[kbl][i], acc[i]);
-#endif
     };
     // barrier of stage s (its DMA landed everywhere, stage s-1's buffer is free) + the DMA of
     // stage s+NS-1 into it
@@ -659,9 +643,7 @@ void dense_lds_kernel(const DenseSplitArgs A) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         stage_barrier();
         if (s < 12) PN2_DSTAMP(1 + s);
-#ifndef PN2_DENSE_DIAG_NODMA  // diagnostic builds only (wrong results): no loads in the loop
         if (s + NS - 1 < nst) issue(s + NS - 1);
-#endif
     };
     // one stage with the next one's entry, reads and split behind its MFMAs
     auto stage_step = [&](int st, const Frags &cur, const Split (&xc)[2], Frags &nxt, Split (&xn)[2]) {

@@ -9,14 +9,14 @@ There is no fallback: if the library is missing or fails to load, every op raise
 """
 import ctypes
 import os
+import threading
 
 import torch  # noqa: F401  (must be loaded before libpn2.so: shared HIP runtime)
 
 from . import tuning
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# tuning key `lib` (PN2_TUNING=lib=...): an alternative build, for A/B experiments only
-LIB_PATH = tuning.get("lib") or os.path.join(_HERE, "libpn2.so")
+LIB_PATH = os.path.join(_HERE, "libpn2.so")
 
 _i64 = ctypes.c_int64
 _int = ctypes.c_int
@@ -112,12 +112,15 @@ SIGNATURES = {
     "pn2_tuning_keys": (ctypes.c_char_p, []),
     "pn2_tuning_local": (_int, [_int]),
     "pn2_device_errors": (_int, [_int, ctypes.POINTER(ctypes.c_uint32)]),
+    "pn2_error_slot_set": (_int, [_vp]),
+    "pn2_error_slot_take": (_int, [_int, ctypes.POINTER(ctypes.c_uint32), _vp]),
+    "pn2_tuning_default": (_int, [ctypes.c_char_p, ctypes.POINTER(_i64)]),
     "pn2_fc_tail_workspace_bytes": (_i64, [_i64, _i64, _i64]),
     "pn2_fc_tail_f32": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64,
                                _int, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 _lib = None
 
 
@@ -148,18 +151,54 @@ def check(rc, what):
         raise Pn2Error("%s failed (code %d): %s" % (what, rc, msg))
 
 
+# ------------------------------------------------------------------ device error slots
+# Each (host thread, device) pair gets its own two-word slot (include/pn2.h pn2_error_slot_set),
+# so a thread's check_device_errors() sees, and clears, only the bits its own launches raised
+# (the reference's mutilthreading/predict_test.py:44-63 runs heads on four threads at once).
+# Slots are never freed: a captured graph keeps raising into its capturing thread's slot.
+_slots_tls = threading.local()
+_slots_keep = []
+_slots_lock = threading.Lock()
+
+
+def bind_error_slot(device):
+    """Make `device`'s launches from this thread raise into this thread's own slot (idempotent:
+    a dict lookup after the first call).  While a stream capture is running no slot can be
+    allocated: the thread then keeps the process-wide default slot until its next call."""
+    idx = device.index if isinstance(device, torch.device) else int(device)
+    if idx is None:
+        idx = torch.cuda.current_device()
+    bound = getattr(_slots_tls, "slots", None)
+    if bound is None:
+        bound = _slots_tls.slots = {}
+    slot = bound.get(idx)
+    if slot is not None:
+        return slot
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    slot = torch.zeros(2, dtype=torch.int32, device="cuda:%d" % idx)
+    torch.cuda.current_stream(idx).synchronize()  # zeroed before any kernel may raise into it
+    with _slots_lock:
+        _slots_keep.append(slot)
+    with torch.cuda.device(idx):
+        check(load().pn2_error_slot_set(slot.data_ptr()), "pn2_error_slot_set")
+    bound[idx] = slot
+    return slot
+
+
 def device_errors(device=None, clear=True):
-    """The device error word (include/pn2.h pn2_device_errors) after the device's queued work:
-    bits DEVERR_*; cleared unless clear=False."""
-    torch.cuda.synchronize(device)
-    prev = torch.cuda.current_device()
-    if device is not None:
-        torch.cuda.set_device(device)
-    try:
-        bits = ctypes.c_uint32(0)
-        check(load().pn2_device_errors(1 if clear else 0, ctypes.byref(bits)), "pn2_device_errors")
-    finally:
-        torch.cuda.set_device(prev)
+    """This thread's device error bits (DEVERR_*) on `device` after the device's queued work,
+    cleared unless clear=False (include/pn2.h pn2_error_slot_take)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    bind_error_slot(dev)
+    torch.cuda.synchronize(dev)  # every stream: this thread's launches may be on any of them
+    bits = ctypes.c_uint32(0)
+    with torch.cuda.device(dev):
+        check(load().pn2_error_slot_take(1 if clear else 0, ctypes.byref(bits),
+                                         torch.cuda.current_stream(dev).cuda_stream),
+              "pn2_error_slot_take")
     return bits.value
 
 
@@ -177,5 +216,7 @@ def check_device_errors(device=None):
 
 
 def stream_ptr(device):
-    """hipStream_t of torch's current stream on `device`, as an int for ctypes."""
+    """hipStream_t of torch's current stream on `device`, as an int for ctypes (and this
+    thread's device error slot bound first: every launch goes through here or ops._stream)."""
+    bind_error_slot(device)
     return torch.cuda.current_stream(device).cuda_stream

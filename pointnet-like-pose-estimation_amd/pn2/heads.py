@@ -60,6 +60,17 @@ class _FCHead(nn.Module):
         x = self.drop(F.relu(self.bn2(self.fc2(x))))
         return self.fc3(x)
 
+    def _mean_mlp(self, mean):
+        """translation_ssg.py:23-33's mean MLP, mean_fc2(relu(mean_bn1(mean_fc1(mean)))).  Eval
+        without autograd: mean_fc1 + mean_bn1 folded, ReLU in the epilogue, then mean_fc2, on
+        pn2_linear_rows_f32 -- a [B, 3] x [3, 6] product is not worth two library GEMM launches
+        and BatchNorm1d's kernels.  Otherwise (or when mean_bn1 cannot fold) the modules."""
+        if not _needs_autograd(self, mean) and mean.is_cuda:
+            c = self._fc_cache
+            h = linear_bn(mean, self.mean_fc1, self.mean_bn1, c.setdefault("mean1", {}))
+            return linear_bn(h, self.mean_fc2, None, c.setdefault("mean2", {}), relu=False)
+        return self.mean_fc2(F.relu(self.mean_bn1(self.mean_fc1(mean))))
+
     def _fc_log_softmax(self, x):
         """(F.log_softmax(fc(x), -1), its first argmax per row): pointnet2_cls_ssg.py:36-38."""
         if self._fused_ok(x):
@@ -146,7 +157,7 @@ class TranslationSSG(_FCHead):
     def forward(self, points, mean):
         B = points.shape[0]
         if self.mean_mlp == 'True':
-            mean = self.mean_fc2(F.relu(self.mean_bn1(self.mean_fc1(mean))))
+            mean = self._mean_mlp(mean)
         l1p, l1f = self.sa1(points, None)
         _, l2f = self.sa2(l1p, l1f)
         return self._fc(l2f.reshape(B, 1024)) + mean
@@ -185,7 +196,7 @@ class TranslationMSG(_FCHead):
     def forward(self, points, mean):
         B = points.shape[0]
         if self.mean_mlp == 'True':
-            mean = self.mean_fc2(F.relu(self.mean_bn1(self.mean_fc1(mean))))
+            mean = self._mean_mlp(mean)
         l1p, l1f = self.sa1(points, None)
         _, l2f = self.sa2(l1p, l1f)
         return self._fc(l2f.reshape(B, 1024)) + mean

@@ -111,7 +111,8 @@ def _dev(t: Tensor, what: str):
 
 
 def _stream(t: Tensor) -> int:
-    return torch.cuda.current_stream(t.device).cuda_stream
+    # this thread's device error slot first (a dict lookup once bound): kernels raise into it
+    return _lib.stream_ptr(t.device)
 
 
 def packed_stride(C: int) -> int:

@@ -187,8 +187,22 @@ class PipelinedForward:
         self.model = model
         self.geometry_cus = geometry_cus
         self.tail = tail
-        self.sas = [m for m in model.modules()
-                    if isinstance(m, (PointNetSetAbstraction, PointNetSetAbstractionMsg))]
+        self.sas = self._find_sas()
+
+    def _find_sas(self):
+        return [m for m in self.model.modules()
+                if isinstance(m, (PointNetSetAbstraction, PointNetSetAbstractionMsg))]
+
+    _GEO_ATTRS = ("point_number", "sample_number", "radius", "group_all", "radius_list",
+                  "sample_number_list")
+
+    def _geo_sig(self):
+        """What the geometry graphs bake in besides the input: each SA module and its sampling /
+        grouping configuration (an in-place change of e.g. ``sa1.radius`` must recapture)."""
+        def frz(v):
+            return tuple(v) if isinstance(v, list) else v
+        return tuple((id(sa),) + tuple(frz(getattr(sa, a, None)) for a in self._GEO_ATTRS)
+                     for sa in self.sas)
 
     @staticmethod
     def _to_tail(tail):
@@ -620,7 +634,7 @@ class GraphedPipeline(PipelinedForward):
         extra_of = (lambda i: ()) if extras is None else (lambda i: tuple(extras[i]))
         from .graphs import ParamState, _sig
         x0, e0 = batches[0], extra_of(0)
-        sig = (_sig((x0,) + tuple(e0)), ops.current_precision())
+        sig = (_sig((x0,) + tuple(e0)), ops.current_precision(), self._geo_sig())
         # the other batches need only the same input signature; a batch list repeating one
         # input needs nothing
         for i in range(1, len(batches)):
@@ -638,7 +652,10 @@ class GraphedPipeline(PipelinedForward):
         # coordinates and draws alone, and the check's host time (a walk over every parameter
         # and buffer, ~40-110 us) then overlaps that group's FPS instead of delaying it.
         check_params = self._slots is not None and sig == self._key
+        rng0 = shard.rng_state() if check_params else None  # see the parameter check below
         if not check_params:
+            self.sas = self._find_sas()
+            sig = sig[:2] + (self._geo_sig(),)
             self._slots = None
             draws = []
 
@@ -747,6 +764,13 @@ class GraphedPipeline(PipelinedForward):
                     check_params = False
                     pk = self._params.key()
                     if pk != self._pkey:
+                        if [id(m) for m in self._find_sas()] != [id(m) for m in self.sas]:
+                            # an SA module was replaced: the geometry graphs are stale too.
+                            # Take back the issued group's draws and start over (full capture)
+                            torch.cuda.synchronize(dev)
+                            shard.set_rng_state(rng0)
+                            self._slots = None
+                            return self.run(batches, extras, post)
                         self._recapture_forwards(extra_of(i), dev)
                         self._pkey = self._params.key()
                 sl = self._slots[s].halves[h]

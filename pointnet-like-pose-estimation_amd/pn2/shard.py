@@ -35,17 +35,49 @@ def batch_shard(global_batch, offset):
         _state.spec = prev
 
 
+@contextlib.contextmanager
+def thread_generator(generator):
+    """Within this context (this host thread) the FPS start draws come from `generator` (a CPU
+    torch.Generator) instead of the CPU default generator.  The reference draws from the
+    default generator (pointnet2_utils.py:59), so forwards running concurrently on several
+    threads (mutilthreading/predict_test.py:44-63) interleave their draws in whatever order
+    the threads happen to run; a generator per thread makes each thread's draws -- and its
+    outputs -- reproducible.  None: the default generator."""
+    prev = getattr(_state, "gen", None)
+    _state.gen = generator
+    try:
+        yield
+    finally:
+        _state.gen = prev
+
+
+def rng_state():
+    """The state of the generator the start draws come from (this thread's thread_generator, or
+    the CPU default generator) -- for a caller that must take draws back (set_rng_state)."""
+    gen = getattr(_state, "gen", None)
+    return gen.get_state() if gen is not None else torch.get_rng_state()
+
+
+def set_rng_state(state):
+    gen = getattr(_state, "gen", None)
+    if gen is not None:
+        gen.set_state(state)
+    else:
+        torch.set_rng_state(state)
+
+
 def draw_start(B, N, pin=True):
     """CPU int64 [B]: the reference's randint draw (or this shard's slice of it), pinned (unless
     pin=False) so the host->device copy is asynchronous."""
     spec = getattr(_state, "spec", None)
+    gen = getattr(_state, "gen", None)
     if spec is None:
-        t = torch.randint(0, N, (B,), dtype=torch.long)
+        t = torch.randint(0, N, (B,), dtype=torch.long, generator=gen)
     else:
         gb, off = spec
         if off + B > gb:
             raise ValueError("batch_shard: shard [%d, %d) outside global batch %d" % (off, off + B, gb))
-        t = torch.randint(0, N, (gb,), dtype=torch.long)[off:off + B]
+        t = torch.randint(0, N, (gb,), dtype=torch.long, generator=gen)[off:off + B]
     return t.pin_memory() if pin and torch.cuda.is_available() else t
 
 
@@ -56,7 +88,7 @@ def draw_start_into(dst, N):
     spec = getattr(_state, "spec", None)
     B = dst.shape[0]
     if spec is None or (spec[0] == B and spec[1] == 0):
-        torch.randint(0, N, (B,), dtype=torch.long, out=dst)
+        torch.randint(0, N, (B,), dtype=torch.long, out=dst, generator=getattr(_state, "gen", None))
     else:
         dst.copy_(draw_start(B, N, pin=False))
 

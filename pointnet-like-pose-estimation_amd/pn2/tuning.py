@@ -6,11 +6,10 @@ The product path reads one environment variable, once, at import:
 
 Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_set``:
 ``mlp_f32``, ``chain_prepass``, ``compact``, ``compact_pool``, ``compact_stages``,
-``bq_waves``, ``bq_rowbuf_kb``, ``fps_threads``, ``fps_ppt``, ``fps_mid``, ``fps_cull``, ``dense_maxntc``,
+``bq_waves``, ``bq_rowbuf_kb``, ``fps_threads``, ``fps_ppt``, ``fps_mid``, ``dense_maxntc``,
 ``dense_minwg``, ``dense_wide_minwg``, ``dense_lds``, ``dense_lds_stages``, ``dense_lds_xcd2d``,
 ``dense_lds_tile``; csrc/pn2_internal.h documents each) and these host-side ones:
 
-    lib              path of an alternative libpn2.so build (A/B builds)
     tail_prio        1: the pipeline's tail stream at high priority
     heads_on_compute 1: the pipeline's heads on the compute streams, no tail stream
     pipe_split_last  1: the pipeline's compute/tail split after the last SA layer
@@ -31,13 +30,15 @@ Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_s
                      eager forward, GraphedForward); 0: the defaults everywhere
 
 Unknown keys are an error.  ``override(**kw)`` changes keys for the duration of a ``with``
-block (tests).  Every default is the measured best.
+block (tests); process-wide kernel keys are atomic words in the library, so a change on one
+thread while another launches is safe.  ``pipeline_profile()`` applies PIPELINE_PROFILE only
+to keys still at their library default: an explicit setting wins inside the pipelines too.
+Every default is the measured best.
 """
 import contextlib
 import os
 
 HOST_DEFAULTS = {
-    "lib": "",
     "pipe_profile": 1,
     "tail_prio": 0,
     "heads_on_compute": 0,
@@ -57,7 +58,7 @@ def _parse(text):
         if "=" not in item:
             raise ValueError("PN2_TUNING: expected key=value, got %r" % item)
         k, v = (s.strip() for s in item.split("=", 1))
-        out[k] = v if k == "lib" else int(v)
+        out[k] = int(v)
     return out
 
 
@@ -85,14 +86,38 @@ def local():
         _lib.check(L.pn2_tuning_local(0), "pn2_tuning_local")
 
 
+_DEFAULTS = {}
+
+
+def kernel_default(key):
+    """A kernel-selection parameter's library default (pn2_tuning_default)."""
+    if key not in _DEFAULTS:
+        import ctypes
+        from . import _lib
+        v = ctypes.c_int64(0)
+        _lib.check(_lib.load().pn2_tuning_default(key.encode(), ctypes.byref(v)), "pn2_tuning_default")
+        _DEFAULTS[key] = v.value
+    return _DEFAULTS[key]
+
+
+def effective_pipeline_profile():
+    """The PIPELINE_PROFILE entries a pipeline applies now: only keys that still hold their
+    library default -- a key set by PN2_TUNING or override() keeps that value in the pipelines
+    too (an A/B of e.g. dense_lds=1 measures the pipelines as well).  {} with pipe_profile 0."""
+    if not _host["pipe_profile"]:
+        return {}
+    return {k: v for k, v in PIPELINE_PROFILE.items() if kernel(k) == kernel_default(k)}
+
+
 @contextlib.contextmanager
 def pipeline_profile():
-    """Context: PIPELINE_PROFILE applied (when pipe_profile is on) on this thread's own copy of
+    """Context: the effective PIPELINE_PROFILE (above) applied on this thread's own copy of
     the keys -- a forward on another host thread meanwhile keeps the defaults."""
-    if not _host["pipe_profile"]:
+    prof = effective_pipeline_profile()
+    if not prof:
         yield
         return
-    with local(), override(**PIPELINE_PROFILE):
+    with local(), override(**prof):
         yield
 
 

@@ -183,3 +183,112 @@ def test_tuning_local_is_per_thread():
     t.join(10)
     assert seen == {"nested": 256, "worker": 256, "main": base, "after": base}
     assert base == 512
+
+
+def test_pipeline_profile_keeps_explicit_keys():
+    """An explicitly set kernel key wins inside the pipelines' launch profile: the
+    profile only replaces keys still at their library default."""
+    from pn2 import tuning
+    assert tuning.kernel_default("fps_mid") == 512 and tuning.kernel_default("dense_lds") == 1
+    with tuning.pipeline_profile():
+        assert tuning.kernel("fps_mid") == 256 and tuning.kernel("dense_lds") == 0
+    with tuning.override(fps_mid=384):
+        assert tuning.effective_pipeline_profile() == {"dense_lds": 0, "bq_waves": 0}
+        with tuning.pipeline_profile():
+            assert tuning.kernel("fps_mid") == 384 and tuning.kernel("dense_lds") == 0
+    with tuning.override(pipe_profile=0):
+        assert tuning.effective_pipeline_profile() == {}
+
+
+def test_tuning_keys_atomic_under_threads():
+    """Process-wide kernel keys are atomic words (errors.cpp): concurrent sets and gets from
+    several threads always read one of the values written, never a torn one."""
+    import threading
+    from pn2 import _lib, tuning
+    L = _lib.load()
+    base = tuning.kernel("dense_minwg")
+    vals = {base, (1 << 40) + 7, -(1 << 33)}
+    bad = []
+
+    def work(v):
+        for _ in range(2000):
+            tuning._set_kernel(L, "dense_minwg", v)
+            got = tuning.kernel("dense_minwg")
+            if got not in vals:
+                bad.append(got)
+    ts = [threading.Thread(target=work, args=(v,)) for v in vals]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    tuning._set_kernel(L, "dense_minwg", base)
+    assert not bad
+
+
+def test_thread_generator_draws_are_per_thread():
+    """pn2.shard.thread_generator: a thread's FPS start draws come from its own generator, so
+    concurrent threads draw reproducibly; outside it the CPU default generator (the reference's)."""
+    import threading
+    import torch
+    from pn2 import shard
+    g = torch.Generator().manual_seed(5)
+    want = torch.randint(0, 1000, (6,), generator=g)
+    want_into = torch.randint(0, 1000, (6,), generator=g)
+    got = {}
+
+    def work(k):
+        with shard.thread_generator(torch.Generator().manual_seed(5)):
+            got[k] = shard.draw_start(6, 1000, pin=False)
+            dst = torch.empty(6, dtype=torch.long)
+            shard.draw_start_into(dst, 1000)
+            got[k, "into"] = dst
+    torch.manual_seed(1)
+    ref_default = torch.randint(0, 1000, (6,))
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for k in range(4):
+        assert torch.equal(got[k], want) and torch.equal(got[k, "into"], want_into)
+    torch.manual_seed(1)
+    assert torch.equal(shard.draw_start(6, 1000, pin=False), ref_default)
+
+
+def test_error_slot_api_exported():
+    """ABI 14: per-thread device error slots and the tuning defaults are exported."""
+    from pn2 import _lib
+    L = _lib.load()
+    for name in ("pn2_error_slot_set", "pn2_error_slot_take", "pn2_device_errors",
+                 "pn2_tuning_default"):
+        assert hasattr(L, name)
+    import ctypes
+    v = ctypes.c_int64(0)
+    assert L.pn2_tuning_default(b"no_such_key", ctypes.byref(v)) != 0
+
+
+def test_asm_read_checker_flags_violations():
+    """tools/check_asm_reads.py (run by the build on sa_chain.hip's device assembly) flags a
+    pending inline-asm LDS read whose registers are touched, or carried across a branch to a
+    target that does not wait, before its s_waitcnt; and accepts the covered forms."""
+    import importlib.util
+    import io
+    spec = importlib.util.spec_from_file_location("car", os.path.join(ROOT, "tools", "check_asm_reads.py"))
+    car = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(car)
+    head = "_ZN3pn215sa_chain_kernelILi1EEEvv:\n"
+    rd = ";;#ASMSTART\nds_read_b128 v[4:7], v1\n;;#ASMEND\n"
+    tail = ".Lfunc_end0:\n"
+    ok = head + rd + "s_waitcnt lgkmcnt(0)\nv_mov_b32 v9, v5\n" + tail
+    touch = head + rd + "v_mov_b32 v9, v5\ns_waitcnt lgkmcnt(0)\n" + tail
+    younger = head + "ds_read_b32 v20, v2\n" + rd + "s_waitcnt lgkmcnt(1)\nv_mov_b32 v9, v6\n" + tail
+    covered = head + rd + "ds_read_b32 v20, v2\ns_waitcnt lgkmcnt(0)\nv_mov_b32 v9, v6\n" + tail
+    br_bad = head + rd + "s_cbranch_scc1 .LBB0_2\ns_waitcnt lgkmcnt(0)\n.LBB0_2:\nv_mov_b32 v9, v1\n" + tail
+    br_ok = head + rd + "s_cbranch_scc1 .LBB0_2\ns_waitcnt lgkmcnt(0)\n.LBB0_2:\ns_waitcnt lgkmcnt(0)\n" + tail
+    sink = io.StringIO()
+    assert car.check(ok, sink) == 0
+    assert car.check(touch, sink) == 1
+    assert car.check(younger, sink) == 1
+    assert car.check(covered, sink) == 0
+    assert car.check(br_bad, sink) == 1
+    assert car.check(br_ok, sink) == 0

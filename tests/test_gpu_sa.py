@@ -504,3 +504,51 @@ def test_graphed_pipeline_ball_query_in_forward_matches_eager(head):
     for i, (g, w) in enumerate(zip(got, want)):
         for k, (a, b) in enumerate(zip(g, w)):
             np.testing.assert_array_equal(a, b, err_msg="output %d of batch %d" % (k, i))
+
+
+def test_graphed_pipeline_recaptures_geometry_on_sa_change():
+    """the geometry graphs bake in each SA module's sampling / grouping
+    configuration.  Replacing sa1 by a module with another radius, or changing sa2's radius in
+    place, between pipelined runs recaptures them: the results equal the eager forwards', and
+    the CPU generator walks as the eager sequence walks it."""
+    from pn2 import heads as H
+    from pn2.pipeline import GraphedPipeline
+    from pn2.pointnet2_utils import PointNetSetAbstraction as SA
+    torch.manual_seed(9)
+    model = H.ClsSSG().eval()
+    cases.randomize_bn(model, 9)
+    model = model.to(DEV)
+    B, N = 8, 1024
+    xs = [cases.cloud("uniform3", B, N, 70 + i).permute(0, 2, 1).contiguous().to(DEV) for i in range(4)]
+
+    def check(gp):
+        torch.manual_seed(12)
+        with torch.no_grad():
+            want = [model(x)[1].cpu() for x in xs]
+        rng_want = torch.randint(0, 1 << 30, (4,))
+        torch.manual_seed(12)
+        got = [o[1].cpu() for o in gp.run(xs)]
+        assert torch.equal(torch.randint(0, 1 << 30, (4,)), rng_want)
+        for i, (g, w) in enumerate(zip(got, want)):
+            assert torch.equal(g, w), "batch %d" % i
+
+    gp = GraphedPipeline(model)
+    check(gp)
+    slots = gp._slots
+    check(gp)
+    assert gp._slots is slots  # replayed
+
+    # a replaced module (new identity, another radius): found by the parameter check, the run
+    # restarts with a full capture
+    torch.manual_seed(3)
+    new = SA(512, 32, 0.3, 3, [64, 64, 128], False).eval()
+    cases.randomize_bn(new, 3)
+    model.sa1 = new.to(DEV)
+    check(gp)
+    assert gp._slots is not slots and gp.sas[0] is model.sa1
+    slots = gp._slots
+
+    # an in-place change of a module's grouping: found by the input signature
+    model.sa2.radius = 0.5
+    check(gp)
+    assert gp._slots is not slots

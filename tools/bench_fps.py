@@ -2,7 +2,7 @@
 BASELINE geometries, checking every variant against the CPU oracle first.  Prints one line per
 (shape, variant): microseconds per launch and per serial iteration.
     python tools/bench_fps.py [--default-only] [--tag NAME] [--shapes=ssg_sa1,...] [--variants=256x4,...]
-(PN2_TUNING=lib=<path> times another build of the library.)"""
+(PN2_DEBUG_LIB=<path> times another build of the library.)"""
 import json
 import os
 import sys
@@ -15,6 +15,9 @@ import torch  # noqa: E402
 
 import cases  # noqa: E402
 import oracle  # noqa: E402
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "debug"))
+import varlib  # noqa: E402
+varlib.setup()
 import pn2  # noqa: E402
 
 SHAPES = [  # (name, B, N, C, S, kind)
@@ -27,15 +30,6 @@ SHAPES = [  # (name, B, N, C, S, kind)
 ]
 VARIANTS = ["64x4", "64x8", "64x16", "128x4", "128x8", "256x2", "256x4", "512x2", "512x4", "1024x1",
             "1024x2", "1024x4", "1024x8", "1024x16", ""]
-
-
-def _cull_points(f):
-    """points per block of a forced culled shape NT*100 + Q*10 + PPC (Q may exceed 9)"""
-    for nt in (1024, 512, 256):
-        r = f - nt * 100
-        if 0 <= r < 1000:
-            return nt * (r // 10) * (r % 10)
-    return 0
 
 
 def main():
@@ -54,19 +48,12 @@ def main():
         sd = start.to(dev)
         want = oracle.farthest_point_sample(x[:2], S, start[:2])
         only = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--variants=")]
-        culls = [a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--cull=")]
-        todo = [(v, 1) for v in (only[0] if only else [""] if only_default else VARIANTS)]
-        if culls:  # fps_cull values (0: index-ordered kernel, 1: default culled shape, NT*100+Q*10+PPC)
-            todo = [("", int(cv)) for cv in culls[0]]
-        for v, cull in todo:
+        todo = only[0] if only else [""] if only_default else VARIANTS
+        for v in todo:
             nt, ppt = map(int, v.split("x")) if v else (0, 0)
             if v and (nt * ppt < N or (nt * ppt >= 4 * N and not only)):
                 continue
-            if cull > 1 and _cull_points(cull) < N:
-                continue
-            if v == "" and cull != 1:
-                v = "cull=%d" % cull
-            with tuning.override(fps_threads=nt, fps_ppt=ppt, fps_cull=cull):
+            with tuning.override(fps_threads=nt, fps_ppt=ppt):
                 idx = torch.ops.pn2.fps(xd, S, sd)[0]
                 ok = bool((idx[:2].cpu().numpy() == want).all())
                 torch.cuda.synchronize()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Diagnostic build: libpn2 with timeline stamps in the SA chain kernel (-DPN2_CHAIN_STAMPS)
-# -> pointnet-like-pose-estimation_amd/pn2/var/stamps.so (load with PN2_TUNING=lib=...)
+# -> pointnet-like-pose-estimation_amd/pn2/var/stamps.so (load with PN2_DEBUG_LIB=...)
 set -eu
 cd "$(dirname "$0")/../../pointnet-like-pose-estimation_amd"
 OUT=build/stamps

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B build: libpn2 with one source compiled with extra flags -> pn2/var/<name>.so
-#   bash tools/debug/build_var.sh <name> <source.hip> <flags...>   (load with PN2_TUNING=lib=...)
+#   bash tools/debug/build_var.sh <name> <source.hip> <flags...>   (load with PN2_DEBUG_LIB=...)
 set -eu
 name=$1; src=$2; shift 2
 cd "$(dirname "$0")/../../pointnet-like-pose-estimation_amd"

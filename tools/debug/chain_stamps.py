@@ -1,5 +1,5 @@
 """Per-workgroup timeline of the SA chain kernel (diagnostic build, tools/debug/build_stamps.sh):
-PN2_TUNING=lib=.../pn2/var/stamps.so python tools/debug/chain_stamps.py
+PN2_DEBUG_LIB=.../pn2/var/stamps.so python tools/debug/chain_stamps.py
 Runs the SSG B=32 N=1024 sa1 and sa2 layers once each (eager, after warm-up) and prints, per
 layer: kernel span, workgroups that did work / left early, percentiles of each phase
 (setup = entry -> BN staged, layer 0 incl. gather, layer 1, layer 2 + pooling, write-out)
@@ -15,6 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, os.path.join(ROOT, "pointnet-like-pose-estimation_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 import cases  # noqa: E402
+import varlib  # noqa: E402
+varlib.setup()
 from pn2 import _lib  # noqa: E402
 from pn2 import heads as H  # noqa: E402
 

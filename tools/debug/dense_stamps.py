@@ -1,5 +1,5 @@
 """Per-workgroup timeline of the dense layer kernel (diagnostic build,
-tools/debug/build_dense_stamps.sh): PN2_TUNING=lib=.../pn2/var/dstamps.so python tools/debug/dense_stamps.py
+tools/debug/build_dense_stamps.sh): PN2_DEBUG_LIB=.../pn2/var/dstamps.so python tools/debug/dense_stamps.py
 Runs one eager SSG B=32 N=1024 forward after warm-up; the last dense launch of it is sa3's
 512 -> 1024 layer (group_all, pooled over the 128 points of a cloud); CONFIG=pose: translation_ssg's
 sa2 512 -> 1024 layer at B=64 (GRID=1024 wide tiles, NST=8).  Prints the spread of
@@ -16,6 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, os.path.join(ROOT, "pointnet-like-pose-estimation_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 import cases  # noqa: E402
+import varlib  # noqa: E402
+varlib.setup()
 from pn2 import _lib  # noqa: E402
 from pn2 import heads as H  # noqa: E402
 

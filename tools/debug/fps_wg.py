@@ -1,5 +1,5 @@
 """Per-workgroup entry / exit times of the FPS launches inside the pipelined SSG run (diagnostic
-build with -DPN2_FPS_WGSTAMPS, load with PN2_TUNING=lib=...):
+build with -DPN2_FPS_WGSTAMPS, load with PN2_DEBUG_LIB=...):
     python tools/debug/fps_wg.py [K]
 Every geometry group launches FPS sa1 then FPS sa2, 64 workgroups each (2 batches x 32 clouds).
 Prints per launch the spread of the workgroups' start times (how long the launch waited for
@@ -15,6 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, os.path.join(ROOT, "pointnet-like-pose-estimation_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 import cases  # noqa: E402
+import varlib  # noqa: E402
+varlib.setup()
 from pn2 import _lib  # noqa: E402
 from pn2 import heads as H  # noqa: E402
 from pn2.pipeline import GraphedPipeline  # noqa: E402
