@@ -60,7 +60,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 14
+#define PN2_ABI_VERSION 15
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -215,9 +215,12 @@ typedef struct pn2_mlp_layer {
  * flags argument. */
 #define PN2_LAYER_NO_RELU 1
 
-/* The same W packed for the split-bf16 chain kernel: three bf16 planes (hi, mid, lo with
- * W = hi + mid + lo to 2^-24 relative), each [cout/32][kblocks][64 lanes][8] in MFMA fragment
- * order.  Kernel input channel k (block k/16) maps to W's input channel as follows:
+/* The same W packed for the split chain / dense kernels.  Planes 0-2: three bf16 planes (hi, mid,
+ * lo with W = hi + mid + lo to 2^-24 relative), each [cout/32][kblocks][64 lanes][8] in MFMA
+ * fragment order; planes 3-4: two fp16 planes (hi, lo) of W[o][.] * 2^e_o in the same order,
+ * e_o putting output row o's largest |w| in [2^14, 2^15) (W*2^e = hi + lo to 2^-22 relative);
+ * then float [cout] = 2^-e_o.  Kernel input channel k (block k/16) maps to W's input channel as
+ * follows:
  *   xyz == 0 (hidden layers): k.   xyz > 0 (first layer, rows [xyz | features], D = cin-xyz):
  *   block 0 holds the xyz channels (k < xyz), blocks >= 1 the features (k-16 < D); W's own
  *   order is [xyz, features] if xyz_first (sample_and_group) else [features, xyz] (MSG).
@@ -225,8 +228,10 @@ typedef struct pn2_mlp_layer {
  * (0 for padding).  kblocks = pn2_layer_split_kblocks(cin, xyz); the image takes
  * pn2_layer_split_bytes(cout, cin, xyz) bytes, 16-byte aligned.  Chains given wt_split for
  * every layer (3 layers, grouped rows, hidden widths 32..128) run as one register-resident
- * kernel with fp32-accurate 6-product bf16 MFMA arithmetic; others (and tuning mlp_f32 = 1)
- * use the fp32 MFMA kernels. */
+ * kernel with fp32-accurate arithmetic: split fp16 (3 MFMAs per product, both operands scaled
+ * by powers of two) where the chain's layer-0 input is register-resident or pre-transformed,
+ * else split bf16 (6 MFMAs per product); others (and tuning mlp_f32 = 1) use the fp32 MFMA
+ * kernels. */
 int64_t pn2_layer_split_kblocks(int64_t cin, int64_t xyz);
 int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin, int64_t xyz);
 int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t xyz,
@@ -371,6 +376,9 @@ int pn2_fc_tail_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const flo
 #define PN2_PATH_SPLIT_BF16 2
 #define PN2_PATH_BF16 3
 int pn2_sa_mlp_last_path(void);
+/* Planes per operand of this thread's last register-resident chain launch: 3 (split bf16),
+ * 2 (split fp16), 1 (bf16); 0 before any. */
+int pn2_sa_mlp_last_planes(void);
 
 /* ---- runtime: CU-partitioned streams (pipelined serving, pn2/pipeline.py) ---- */
 int pn2_device_cu_count(int device, int *count);

@@ -35,6 +35,8 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
 // the one PN2_TUNING variable).  X(name, default)
 #define PN2_TUNING_KEYS(X)                                                                     \
     X(mlp_f32, 0)          /* 1: fp32 MFMA kernels instead of the split-bf16 ones          */ \
+    X(chain_f16, 1)        /* 1: fp32-accurate chains as split fp16 (3 MFMAs per product)   */ \
+                           /* where eligible; 0: split bf16 (6)                             */ \
     X(chain_prepass, 1)    /* 0: no layer-0 pre-pass (wide first layers of a chain)        */ \
     X(compact, 1)          /* 0: no compact neighbourhoods (every padded row computed)     */ \
     X(compact_pool, 16)     /* LDS pool rows of compact chain launches (0: automatic)       */ \

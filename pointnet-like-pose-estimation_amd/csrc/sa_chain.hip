@@ -44,9 +44,10 @@ constexpr int kChainWaves = 4;
 constexpr int kChainRows = 32 * kChainWaves;
 
 struct ChainLayer {
-    const bf16x8 *w;  // [3][tiles][kb][64] fragments
+    const bf16x8 *w;  // [NP][tiles][kb][64] fragments
     const float *alpha;
     const float *beta;
+    const float *wscale;  // NP = 2: per output channel, the inverse of the weight row's scale
     int kb;     // 16-deep k blocks of the input
     int tiles;  // 32-wide output tiles
 };
@@ -122,22 +123,24 @@ __device__ __forceinline__ Split load_w(const ChainLayer &L, int t, int kb, int 
     const bf16x8 *p = L.w + ((int64_t)t * L.kb + kb) * 64 + lane;
     Split s;
     s.h = p[0];
-    s.m = NP == 3 ? p[plane] : s.h;
+    s.m = NP >= 2 ? p[plane] : s.h;
     s.l = NP == 3 ? p[2 * plane] : s.h;
     return s;
 }
 
 // BN + ReLU of a transposed hidden tile, split into the next layer's k-blocks 2t, 2t+1
 // al/be: this layer's BN scale/shift staged in LDS
+// asc: NP = 2, the down-scale of the layer's input activations (act_scale), else 1
 template <int NP>
 __device__ __forceinline__ void hidden_epilogue(const cfloatx16 &acc, const float *al,
                                                 const float *be, int t, int h, Split &lo,
-                                                Split &hi) {
+                                                Split &hi, float asc = 1.f) {
     cfloatx4 a4[4], b4[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         a4[m] = *reinterpret_cast<const cfloatx4 *>(al + 32 * t + 8 * m + 4 * h);
         b4[m] = *reinterpret_cast<const cfloatx4 *>(be + 32 * t + 8 * m + 4 * h);
+        if constexpr (NP == 2) a4[m] *= asc;
     }
     float y0[8], y1[8];
 #pragma unroll
@@ -160,18 +163,20 @@ struct F8 {
 };
 template <int NP> struct HidT { using type = Split; };
 template <> struct HidT<3> { using type = F8; };
+template <> struct HidT<2> { using type = F8; };  // (split after the wave's scale is known)
 
 template <int NP>
 __device__ __forceinline__ void hidden_epilogue_h(const cfloatx16 &acc, const float *al,
                                                   const float *be, int t, int h,
                                                   typename HidT<NP>::type &lo,
-                                                  typename HidT<NP>::type &hi) {
-    if constexpr (NP == 3) {
+                                                  typename HidT<NP>::type &hi, float asc = 1.f) {
+    if constexpr (NP >= 2) {
         cfloatx4 a4[4], b4[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             a4[m] = *reinterpret_cast<const cfloatx4 *>(al + 32 * t + 8 * m + 4 * h);
             b4[m] = *reinterpret_cast<const cfloatx4 *>(be + 32 * t + 8 * m + 4 * h);
+            if constexpr (NP == 2) a4[m] *= asc;
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -183,11 +188,24 @@ __device__ __forceinline__ void hidden_epilogue_h(const cfloatx16 &acc, const fl
     }
 }
 template <int NP>
-__device__ __forceinline__ Split hid_split(const Split &x) { return x; }
+__device__ __forceinline__ Split hid_split(const Split &x, float = 1.f) { return x; }
 template <int NP>
-__device__ __forceinline__ Split hid_split(const F8 &x) {
-    return splitN<NP>(x.v);
+__device__ __forceinline__ Split hid_split(const F8 &x, float up = 1.f) {
+    if constexpr (NP == 2) {
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = x.v[j] * up;
+        return splitN<NP>(y);
+    } else {
+        return splitN<NP>(x.v);
+    }
 }
+// NP = 2: the wave-uniform scale of a set of activations from the lane's running max of their
+// magnitudes (as uint bits: order-preserving for values >= +0)
+__device__ __forceinline__ ActScale wave_act_scale(unsigned lane_max_bits) {
+    return act_scale(__uint_as_float(wave_max_u32(lane_max_bits)));
+}
+__device__ __forceinline__ unsigned mag_bits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
 __device__ __forceinline__ unsigned hid_dep(const Split &x) {
     return __builtin_bit_cast(unsigned, __builtin_shufflevector(x.h, x.h, 0, 1));
 }
@@ -199,6 +217,8 @@ template <int NP>
 __device__ __forceinline__ void pin_pair(Split &a, Split &b) {
     if constexpr (NP == 3)
         asm volatile("" : "+v"(a.h), "+v"(a.m), "+v"(a.l), "+v"(b.h), "+v"(b.m), "+v"(b.l));
+    else if constexpr (NP == 2)
+        asm volatile("" : "+v"(a.h), "+v"(a.m), "+v"(b.h), "+v"(b.m));
     else
         asm volatile("" : "+v"(a.h), "+v"(b.h));
 }
@@ -246,6 +266,7 @@ __device__ __forceinline__ void stage_wait() {
     static_assert(KS == 2 || KS == 3, "stage_wait count");
     if constexpr (KS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if constexpr (NP == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if constexpr (NP == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
 }
 
@@ -308,15 +329,21 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     float *al2 = be1 + 32 * T1, *be2 = al2 + coutL;
     const bool bnreg = coutL <= 2 * 64 * kChainWaves;  // every thread's share fits 8 registers
     float bnv[8];
+    // NP = 2: the BN scale of a layer whose products run on the chain's MFMAs takes the inverse
+    // of the weight rows' scale (split_bf16.h); a pre-transformed layer 0 has none (wscale null)
+    auto alpha_of = [&](const ChainLayer &L, int c) {
+        if constexpr (NP == 2) return L.wscale ? L.alpha[c] * L.wscale[c] : L.alpha[c];
+        else return L.alpha[c];
+    };
     if (bnreg) {
         const int e2 = tid + 64 * kChainWaves;
-        bnv[0] = tid < 32 * T0 ? L0.alpha[tid] : 0.f;
+        bnv[0] = tid < 32 * T0 ? alpha_of(L0, tid) : 0.f;
         bnv[1] = tid < 32 * T0 ? L0.beta[tid] : 0.f;
-        bnv[2] = tid < 32 * T1 ? L1.alpha[tid] : 0.f;
+        bnv[2] = tid < 32 * T1 ? alpha_of(L1, tid) : 0.f;
         bnv[3] = tid < 32 * T1 ? L1.beta[tid] : 0.f;
-        bnv[4] = tid < coutL ? L2.alpha[tid] : 0.f;
+        bnv[4] = tid < coutL ? alpha_of(L2, tid) : 0.f;
         bnv[5] = tid < coutL ? L2.beta[tid] : 0.f;
-        bnv[6] = e2 < coutL ? L2.alpha[e2] : 0.f;
+        bnv[6] = e2 < coutL ? alpha_of(L2, e2) : 0.f;
         bnv[7] = e2 < coutL ? L2.beta[e2] : 0.f;
     }
 
@@ -387,7 +414,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
 #ifndef PN2_CHAIN_ASMR
 #define PN2_CHAIN_ASMR 1
 #endif
-    constexpr bool ASMR = PN2_CHAIN_ASMR && NP == 3 && (KB0M == 1 || KB0M < 0);
+    constexpr bool ASMR = PN2_CHAIN_ASMR && NP >= 2 && (KB0M == 1 || KB0M < 0);
     Split WB[2];
     int nr = 0;  // ASMR: the next step to read
     const unsigned ring3 = (unsigned)(size_t)(__attribute__((address_space(3))) char *)ring;
@@ -400,13 +427,25 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
         const unsigned a = ring3 + (unsigned)(((nr / kChainWaves) % KS) * kStageBytes +
                                               (nr & (kChainWaves - 1)) * kStepBytes) + loff;
-        asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:1024\n\tds_read_b128 %2, %3 offset:2048"
-                     : "=&v"(w.h), "=&v"(w.m), "=&v"(w.l)
-                     : "v"(a));
+        if constexpr (NP == 3)
+            asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:1024\n\tds_read_b128 %2, %3 offset:2048"
+                         : "=&v"(w.h), "=&v"(w.m), "=&v"(w.l)
+                         : "v"(a));
+        else
+            asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024"
+                         : "=&v"(w.h), "=&v"(w.m)
+                         : "v"(a));
         ++nr;
     };
-    auto wt3 = [&](Split &w) { asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(w.h), "+v"(w.m), "+v"(w.l)); };
-    auto wt0 = [&](Split &w) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w.h), "+v"(w.m), "+v"(w.l)); };
+    // wait for this step's reads; the next step's NP reads (issued after them) may stay in flight
+    auto wt3 = [&](Split &w) {
+        if constexpr (NP == 3) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(w.h), "+v"(w.m), "+v"(w.l));
+        else asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(w.h), "+v"(w.m));
+    };
+    auto wt0 = [&](Split &w) {
+        if constexpr (NP == 3) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w.h), "+v"(w.m), "+v"(w.l));
+        else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(w.h), "+v"(w.m));
+    };
     constexpr int P0 = KB0M > 0 ? T0 * KB0M : 0;  // ASMR layer-0 steps (L0.kb == KB0M == 1)
     constexpr int P1 = P0 + T1 * KB1;              // steps before layer 2
 
@@ -508,9 +547,9 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         if (tid < coutL) { al2[tid] = bnv[4]; be2[tid] = bnv[5]; }
         if (e2 < coutL) { al2[e2] = bnv[6]; be2[e2] = bnv[7]; }
     } else {
-        for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = L2.alpha[e]; be2[e] = L2.beta[e]; }
-        for (int e = tid; e < 32 * T0; e += 64 * kChainWaves) { al0[e] = L0.alpha[e]; be0[e] = L0.beta[e]; }
-        for (int e = tid; e < 32 * T1; e += 64 * kChainWaves) { al1[e] = L1.alpha[e]; be1[e] = L1.beta[e]; }
+        for (int e = tid; e < coutL; e += 64 * kChainWaves) { al2[e] = alpha_of(L2, e); be2[e] = L2.beta[e]; }
+        for (int e = tid; e < 32 * T0; e += 64 * kChainWaves) { al0[e] = alpha_of(L0, e); be0[e] = L0.beta[e]; }
+        for (int e = tid; e < 32 * T1; e += 64 * kChainWaves) { al1[e] = alpha_of(L1, e); be1[e] = L1.beta[e]; }
     }
     if (A.pool_mode == 1 || compact)
         for (int e = tid; e < gpb * coutL; e += 64 * kChainWaves) cpool[e] = 0u;
@@ -568,6 +607,20 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         for (int t = 0; t < T0; ++t)
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+        float asc0 = 1.f;  // NP = 2: the down-scale of layer 0's input
+        if constexpr (NP == 2) {
+            unsigned mb = 0;
+#pragma unroll
+            for (int kb = 0; kb < KB0M; ++kb)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) mb = max(mb, mag_bits(x[kb][j]));
+            const ActScale sc = wave_act_scale(mb);
+#pragma unroll
+            for (int kb = 0; kb < KB0M; ++kb)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[kb][j] *= sc.up;
+            asc0 = sc.down;
+        }
         if constexpr (ASMR) {  // KB0M == 1: one block, T0 steps
             rd(WB[0]);
             const Split xs = splitN<NP>(x[0]);
@@ -589,7 +642,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         }
 #pragma unroll
         for (int t = 0; t < T0; ++t) {
-            hidden_epilogue_h<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1]);
+            hidden_epilogue_h<NP>(acc[t], al0, be0, t, h, X1[2 * t], X1[2 * t + 1], asc0);
             pin_pair<NP>(X1[2 * t], X1[2 * t + 1]);
         }
     } else {
@@ -625,17 +678,30 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     // ---- layer 1: input in registers, k-outer (each input block dies after its use, so X1 and
     // X2 are never both whole in registers), every output tile accumulating (transposed)
     Split X2[2 * T1];
+    float asc2 = 1.f;  // NP = 2: the down-scale of layer 2's input
     {
         cfloatx16 acc[T1];
 #pragma unroll
         for (int t = 0; t < T1; ++t)
 #pragma unroll
             for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+        // NP = 2: one scale for the wave's layer-1 input (ReLU outputs, >= +0)
+        float up1 = 1.f, asc1 = 1.f;
+        if constexpr (NP == 2) {
+            unsigned mb = 0;
+#pragma unroll
+            for (int kb = 0; kb < KB1; ++kb)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) mb = max(mb, __float_as_uint(X1[kb].v[j]));
+            const ActScale sc = wave_act_scale(mb);
+            up1 = sc.up;
+            asc1 = sc.down;
+        }
         if constexpr (ASMR) {
             if constexpr (KB0M < 0) rd(WB[0]);  // (KB0M == 1: layer 0 read this step ahead)
 #pragma unroll
             for (int kb = 0; kb < KB1; ++kb) {
-                const Split xs = hid_split<NP>(X1[kb]);
+                const Split xs = hid_split<NP>(X1[kb], up1);
 #pragma unroll
                 for (int t = 0; t < T1; ++t) {
                     constexpr int dummy = 0;
@@ -649,13 +715,31 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         } else {
 #pragma unroll
             for (int kb = 0; kb < KB1; ++kb) {
-                const Split xs = hid_split<NP>(X1[kb]);
+                const Split xs = hid_split<NP>(X1[kb], up1);
 #pragma unroll
                 for (int t = 0; t < T1; ++t) acc[t] = mma_wa<NP>(next_w(), xs, acc[t]);
             }
         }
+        if constexpr (NP == 2) {
+            // BN + ReLU of every tile in place (fp32), then one scale for the wave's layer-2
+            // input, then the split
+            F8 y[2 * T1];
+            unsigned mb = 0;
 #pragma unroll
-        for (int t = 0; t < T1; ++t) hidden_epilogue<NP>(acc[t], al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
+            for (int t = 0; t < T1; ++t) {
+                hidden_epilogue_h<NP>(acc[t], al1, be1, t, h, y[2 * t], y[2 * t + 1], asc1);
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    mb = max(mb, max(__float_as_uint(y[2 * t].v[j]), __float_as_uint(y[2 * t + 1].v[j])));
+            }
+            const ActScale sc = wave_act_scale(mb);
+            asc2 = sc.down;
+#pragma unroll
+            for (int kb = 0; kb < KB2; ++kb) X2[kb] = hid_split<NP>(y[kb], sc.up);
+        } else {
+#pragma unroll
+            for (int t = 0; t < T1; ++t) hidden_epilogue<NP>(acc[t], al1, be1, t, h, X2[2 * t], X2[2 * t + 1]);
+        }
     }
 
     PN2_STAMP(3);
@@ -682,7 +766,7 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
         // so is relu -- only the row max (al >= 0) or min of the accumulator is needed.
         // Register q of lane half h is row (q&3) + 8(q>>2) + 4h of the slab.
         const int col = 32 * t + r;
-        const float al = al2[col], be = be2[col];
+        const float al = NP == 2 ? al2[col] * asc2 : al2[col], be = be2[col];
         const bool up = al >= 0.f;
         auto fin = [&](float mx, float mn) { return chain_relu(__builtin_fmaf(up ? mx : mn, al, be)); };
         if (compact) {
@@ -813,7 +897,10 @@ using namespace pn2;
 //             W's order is [xyz, features] when xyz_first (sample_and_group, :114), else
 //             [features, xyz] (PointNetSetAbstractionMsg, :209).
 // Fragment element: plane p, tile t, block kb, lane l = 32h + r, element j holds
-//   W[32t + r][in(16kb + (j&3) + 8(j>>2) + 4h)]  split into bf16 planes hi / mid / lo.
+//   W[32t + r][in(16kb + (j&3) + 8(j>>2) + 4h)]  split into bf16 planes hi / mid / lo
+// (planes 0-2), then the same fragments of W[o][.] * 2^e_o split into fp16 planes hi / lo
+// (planes 3-4, the NP = 2 chains: e_o puts the row's largest |w| in [2^14, 2^15)), then the
+// per-row inverse scales 2^-e_o as float [cout] (split_bf16.h).
 __device__ __forceinline__ int split_in_channel(int k, int cin, int xyz, int xyz_first) {
     if (xyz == 0) return k < cin ? k : -1;
     const int D = cin - xyz;
@@ -822,9 +909,27 @@ __device__ __forceinline__ int split_in_channel(int k, int cin, int xyz, int xyz
     return f < D ? (xyz_first ? xyz + f : f) : -1;
 }
 
+// the fp16 image's row scales: 2^e_o with the row's largest |w| * 2^e_o in [2^14, 2^15) (1 for
+// an all-zero row); the image keeps the inverse
+__device__ __forceinline__ float row_scale_exp2(const float *__restrict__ Wrow, int cin, bool inverse) {
+    float m = 0.f;
+    for (int k = 0; k < cin; ++k) m = fmaxf(m, fabsf(Wrow[k]));
+    int e = 0;
+    if (m > 0.f) e = 15 - __builtin_amdgcn_frexp_expf(m);
+    e = e < -100 ? -100 : (e > 100 ? 100 : e);
+    return __uint_as_float((unsigned)(127 + (inverse ? -e : e)) << 23);
+}
+
+__global__ __launch_bounds__(256) void pack_scale_kernel(const float *__restrict__ W, int cout, int cin,
+                                                          float *__restrict__ inv) {
+    const int o = blockIdx.x * 256 + threadIdx.x;
+    if (o < cout) inv[o] = row_scale_exp2(W + (int64_t)o * cin, cin, true);
+}
+
 __global__ __launch_bounds__(256) void pack_split_kernel(const float *__restrict__ W, int cout,
                                                           int cin, int kbs, int xyz, int xyz_first,
-                                                          __bf16 *__restrict__ out) {
+                                                          __bf16 *__restrict__ out,
+                                                          const float *__restrict__ inv) {
     const int64_t per_plane = (int64_t)cout * kbs * 16;
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= per_plane) return;
@@ -842,6 +947,13 @@ __global__ __launch_bounds__(256) void pack_split_kernel(const float *__restrict
     out[e] = a;
     out[per_plane + e] = m;
     out[2 * per_plane + e] = lo;
+    // fp16 planes of the scaled row (inv[] was written by pack_scale_kernel before this launch)
+    const float ws = w * (1.f / inv[32 * t + r]);  // exact: a power of two
+    const _Float16 fh = (_Float16)ws;
+    const _Float16 fl = (_Float16)(ws - (float)fh);
+    _Float16 *o16 = reinterpret_cast<_Float16 *>(out + 3 * per_plane);
+    o16[e] = fh;
+    o16[per_plane + e] = fl;
 }
 
 extern "C" int64_t pn2_layer_split_kblocks(int64_t cin, int64_t xyz) {
@@ -852,8 +964,18 @@ extern "C" int64_t pn2_layer_split_kblocks(int64_t cin, int64_t xyz) {
 extern "C" int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin, int64_t xyz) {
     const int64_t kbs = pn2_layer_split_kblocks(cin, xyz);
     if (cout < 32 || cout % 32 != 0 || kbs < 0) return -1;
-    return 3 * cout * kbs * 16 * 2;
+    return 5 * cout * kbs * 16 * 2 + (cout * 4 + 15) / 16 * 16;
 }
+
+namespace pn2 {
+// the NP = 2 planes and the row scales inside a pn2_pack_layer_split_bf16 image
+static const bf16x8 *split_f16_planes(const void *img, int64_t cout, int64_t kbs) {
+    return reinterpret_cast<const bf16x8 *>(static_cast<const char *>(img) + 3 * cout * kbs * 32);
+}
+static const float *split_f16_inv_scale(const void *img, int64_t cout, int64_t kbs) {
+    return reinterpret_cast<const float *>(static_cast<const char *>(img) + 5 * cout * kbs * 32);
+}
+}  // namespace pn2
 
 extern "C" int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t xyz,
                                          int xyz_first, void *out, void *stream) {
@@ -864,9 +986,13 @@ extern "C" int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t c
                 (long long)cin, (long long)xyz);
     PN2_REQUIRE(((uintptr_t)out & 15) == 0, "pn2_pack_layer_split_bf16: output not 16-byte aligned");
     const int64_t per_plane = cout * kbs * 16;
+    float *inv = const_cast<float *>(split_f16_inv_scale(out, cout, kbs));
+    hipLaunchKernelGGL(pack_scale_kernel, dim3((unsigned)((cout + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), W, (int)cout, (int)cin, inv);
+    PN2_LAUNCH_CHECK("pack_scale_kernel");
     hipLaunchKernelGGL(pack_split_kernel, dim3((unsigned)((per_plane + 255) / 256)), dim3(256), 0,
                        as_stream(stream), W, (int)cout, (int)cin, (int)kbs, (int)xyz, xyz_first ? 1 : 0,
-                       reinterpret_cast<__bf16 *>(out));
+                       reinterpret_cast<__bf16 *>(out), inv);
     PN2_LAUNCH_CHECK("pack_split_kernel");
     return PN2_OK;
 }
@@ -1048,13 +1174,20 @@ extern "C" int pn2_debug_chain_stamps(unsigned long long *dst, int64_t n) {
 
 template <int T0, int T1, int KB0M, int NP>
 static int launch_chain_sig(const ChainArgs &A, unsigned grid, size_t lds, hipStream_t st) {
-    if (A.pool_mode == 3 && A.ks == 2)
-        hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP, 2>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
-    else
-        hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP, kStages>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
-    PN2_LAUNCH_CHECK("sa_chain_kernel");
-    return PN2_OK;
+    if constexpr (NP == 2 && KB0M != 1 && KB0M != -1) {
+        return set_error(PN2_EUNSUPPORTED, "sa_chain: no split-fp16 instance");  // (not reached)
+    } else {
+        if (A.pool_mode == 3 && A.ks == 2)
+            hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP, 2>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
+        else
+            hipLaunchKernelGGL((sa_chain_kernel<T0, T1, KB0M, NP, kStages>), dim3(grid), dim3(64 * kChainWaves), lds, st, A);
+        PN2_LAUNCH_CHECK("sa_chain_kernel");
+        return PN2_OK;
+    }
 }
+
+// planes of the last chain launch on this thread (pn2_sa_mlp_last_planes)
+static thread_local int g_last_planes = 0;
 
 // the compiled KB0M for this chain: the smallest resident bound >= kb0, else 0 (streamed);
 // -1 when (T0, T1) has no instance
@@ -1185,6 +1318,11 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         }
         KB0M = -1;
     }
+    // the fp32-accurate chains run split fp16 (3 MFMAs per product, split_bf16.h) where a whole
+    // layer-0 input is in registers or pre-transformed (the activation scale needs the wave's
+    // whole input); tuning chain_f16 = 0 keeps split bf16 (6 MFMAs)
+    const int npk = (np == 3 && tuning().chain_f16 && (KB0M == 1 || KB0M == -1)) ? 2 : np;
+    const size_t stage_b = npk == 3 ? stage_bytes<3>() : npk == 2 ? stage_bytes<2>() : stage_bytes<1>();
     const int wpc = compact ? (int)compact_wpc(s) : 0;
     // Compact launches: the weight ring's depth against the LDS group pool.  With the full
     // 16-row pool a 3-stage ring cost a workgroup per CU (SSG sa2: 3 -> 2 live per CU, 114 ->
@@ -1200,7 +1338,7 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     if (compact) {
         const int64_t cL = layers[2].cout;
         const size_t bnb = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + cL) + 32;
-        const size_t sb = np == 3 ? stage_bytes<3>() : stage_bytes<1>();
+        const size_t sb = stage_b;
         const int occ_v = T1 >= 4 ? 3 : T1 == 3 ? 4 : 5;  // workgroups per CU the VGPRs allow
         auto wgs = [&](int ks, int prow) {
             return std::min<int64_t>(occ_v, (int64_t)(160 * 1024) / (int64_t)(prow * cL * 4 + bnb + ks * sb));
@@ -1244,6 +1382,10 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         A.L[l].beta = layers[l].beta;
         A.L[l].kb = kbs[l];
         A.L[l].tiles = (int)(layers[l].cout / 32);
+        if (npk == 2 && !(l == 0 && pre)) {  // (a pre-transformed layer 0 runs no MFMA here)
+            A.L[l].w = split_f16_planes(layers[l].wt_split, layers[l].cout, kbs[l]);
+            A.L[l].wscale = split_f16_inv_scale(layers[l].wt_split, layers[l].cout, kbs[l]);
+        }
     }
     A.M = (int)M;
     A.K = (int)K;
@@ -1289,15 +1431,19 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     A.lds_bn = (int)((lds + 15) / 16 * 16);
     const size_t bn_bytes = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + coutL);
     A.lds_ring = (int)((A.lds_bn + bn_bytes + 15) / 16 * 16);
-    lds = (size_t)A.lds_ring + (size_t)(compact ? cks : kStages) * (np == 3 ? stage_bytes<3>() : stage_bytes<1>());
+    lds = (size_t)A.lds_ring + (size_t)(compact ? cks : kStages) * stage_b;
     int rc = PN2_EUNSUPPORTED;
 #define PN2_CHAIN_GO(a, b, c)                                                             \
     if (T0 == a && T1 == b && KB0M == c)                                                  \
-        rc = np == 3 ? launch_chain_sig<a, b, c, 3>(A, grid, lds, st)                     \
-                     : launch_chain_sig<a, b, c, 1>(A, grid, lds, st);
+        rc = npk == 3 ? launch_chain_sig<a, b, c, 3>(A, grid, lds, st)                    \
+           : npk == 2 ? launch_chain_sig<a, b, c, 2>(A, grid, lds, st)                    \
+                      : launch_chain_sig<a, b, c, 1>(A, grid, lds, st);
     PN2_CHAIN_SIGS(PN2_CHAIN_GO)
 #undef PN2_CHAIN_GO
+    if (rc == PN2_OK) g_last_planes = npk;
     return rc == PN2_OK ? 1 : rc;
 }
 
 }  // namespace pn2
+
+extern "C" int pn2_sa_mlp_last_planes(void) { return pn2::g_last_planes; }

@@ -330,8 +330,9 @@ def _(weight, bias, gamma, beta, mean, var, eps, rot):
 
 
 def pack_layer_split_direct(weight: Tensor, xyz: int, xyz_first: bool) -> Tensor:
-    """Conv2d 1x1 weight [cout,cin,1,1] -> the split-bf16 image of pn2_pack_layer_split_bf16
-    (three bf16 planes hi/mid/lo in MFMA fragment order), flat bfloat16.  xyz: the xyz channels
+    """Conv2d 1x1 weight [cout,cin,1,1] -> the split image of pn2_pack_layer_split_bf16 (three
+    bf16 planes hi/mid/lo, two fp16 planes of the row-scaled weights and the rows' inverse
+    scales, in MFMA fragment order), flat 16-bit storage.  xyz: the xyz channels
     of a first layer (its rows are [xyz | features] in the chain kernel; 0 for hidden layers),
     xyz_first: W's own order is [xyz, features] (SSG) rather than [features, xyz] (MSG)."""
     _dev(weight, "pn2::pack_layer_split")
@@ -353,8 +354,7 @@ pack_layer_split = torch.library.custom_op("pn2::pack_layer_split", pack_layer_s
 @pack_layer_split.register_fake
 def _(weight, xyz, xyz_first):
     cout, cin = weight.shape[0], weight.shape[1]
-    kbs = 1 + (cin - xyz + 15) // 16 if xyz else (cin + 15) // 16
-    return weight.new_empty(3 * cout * kbs * 16, dtype=torch.bfloat16)
+    return weight.new_empty(int(_L.pn2_layer_split_bytes(cout, cin, xyz)) // 2, dtype=torch.bfloat16)
 
 
 # ------------------------------------------------------------------------------ sa_mlp_max_

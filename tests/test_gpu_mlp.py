@@ -290,3 +290,78 @@ def test_dense_lds_rows_source_v1():
             outs.append([t.cpu().numpy() for t in (o if isinstance(o, tuple) else (o,)) if t is not None])
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
+
+
+# split-fp16 chains (split_bf16.h NP = 2): accuracy against the float64 oracle, and the power-of-
+# two scaling at extreme magnitudes.  (C, D, K, S, N, radius, mlp, msg, case)
+F16 = [
+    (3, 0, 32, 128, 512, 0.2, [64, 64, 128], False, "plain"),       # SSG sa1: resident layer 0
+    (3, 128, 64, 64, 512, 0.4, [128, 128, 256], False, "plain"),    # SSG sa2: pre-pass layer 0
+    (3, 0, 32, 64, 512, 0.2, [64, 64, 128], False, "coords_1e3"),   # xyz-ctr up to ~200
+    (3, 0, 32, 64, 512, 0.2, [64, 64, 128], False, "coords_1e-4"),  # xyz-ctr ~2e-5
+    (3, 0, 32, 64, 512, 0.2, [64, 64, 128], False, "tiny_row"),     # one weight row 1e-6, var 1e-12
+    (3, 0, 32, 64, 512, 0.2, [64, 64, 128], False, "hidden_1e4"),   # layer-1 inputs ~1e4
+    (3, 0, 32, 64, 512, 0.2, [64, 64, 128], False, "hidden_1e-5"),  # layer-1 inputs ~1e-5
+    (3, 16, 16, 64, 512, 0.3, [32, 32, 64], True, "plain"),         # MSG row order, pre-pass
+]
+
+
+@pytest.mark.parametrize("f16", [1, 0])
+@pytest.mark.parametrize("case", range(len(F16)))
+def test_chain_split_f16_vs_oracle(case, f16):
+    """The fp32-accurate chains run split fp16 (3 MFMAs per product) by default: within 1e-5 of
+    the float64 oracle with margin (the worst error stays below a tenth of the tolerance, as the
+    6-MFMA split bf16 does), including inputs whose magnitudes leave fp16's range unless both
+    operands are scaled: coordinates x1e3 / x1e-4, a weight row of 1e-6 whose BN scale is 1e6,
+    hidden activations ~1e4 / ~1e-5.  f16 = 0: tuning chain_f16 = 0 (split bf16)."""
+    import pn2
+    from pn2 import _lib, tuning
+    C, D, K, S, N, radius, mlp, msg, kind = F16[case]
+    B = 2
+    scale = {"coords_1e3": 1e3, "coords_1e-4": 1e-4}.get(kind, 1.0)
+    pts = cases.cloud("uniform3", B, N, 500 + case) * scale
+    radius = radius * scale
+    gen = torch.Generator().manual_seed(600 + case)
+    feat = torch.randn(B, N, D, generator=gen) if D else None
+    torch.manual_seed(700 + case)
+    if msg:
+        sa = pn2.PointNetSetAbstractionMsg(S, [K], [radius], D, [mlp])
+        convs, bns = sa.conv_blocks[0], sa.bn_blocks[0]
+    else:
+        sa = pn2.PointNetSetAbstraction(S, K, radius, C + D, mlp)
+        convs, bns = sa.mlp_convs, sa.mlp_bns
+    cases.randomize_bn(sa, 800 + case)
+    with torch.no_grad():
+        if kind == "tiny_row":
+            convs[1].weight[5] *= 1e-6
+            convs[1].bias[5] *= 1e-6
+            bns[1].running_mean[5] *= 1e-6
+            bns[1].running_var[5] = 1e-12
+        if kind == "hidden_1e4":
+            bns[0].bias.add_(1e4)
+        if kind == "hidden_1e-5":
+            bns[0].weight.mul_(1e-5)
+            bns[0].bias.mul_(1e-5)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous()
+    f = feat.permute(0, 2, 1).contiguous() if D else None
+    with tuning.override(chain_f16=f16):
+        torch.manual_seed(900 + case)
+        with torch.no_grad():
+            newp, newf = sa(x.to(DEV), None if f is None else f.to(DEV))
+        torch.cuda.synchronize()
+    assert _lib.load().pn2_sa_mlp_last_path() == _lib.PATH_SPLIT_BF16
+    assert _lib.load().pn2_sa_mlp_last_planes() == (2 if f16 else 3)
+    ps = x.permute(0, 2, 1)
+    torch.manual_seed(900 + case)
+    start = torch.randint(0, N, (B,), dtype=torch.long)
+    fi = oracle.farthest_point_sample(ps, S, start)
+    ctr = oracle.index_points(ps, fi)
+    idx = oracle.query_ball_point(radius, K, ps, ctr)
+    grouped = oracle.group(ps, feat, idx, ctr, feature_first=msg)
+    want = oracle.mlp_max(grouped, _oracle_layers(convs, bns))
+    got = newf.permute(0, 2, 1).cpu().numpy().astype(np.float64)
+    tol = 1e-5 * np.abs(want) + 1e-5 * np.abs(want).max()
+    ratio = float((np.abs(got - want) / tol).max())
+    print("case %d %s f16=%d: max err / tol %.4f" % (case, kind, f16, ratio))
+    assert ratio < 0.1
