@@ -20,10 +20,12 @@ JSON line (contract in the task statement) with:
                 dense_split_kernel): achieved = algorithmic fp32 FLOPs (2*M*sum(cin*cout) per
                 call, cin unpadded) / call duration timed with HIP events on the launch stream,
                 over a further K eager steps (kernel durations are launch-mode independent;
-                profiles/ has the rocprofv3 check).  The products run as split-bf16 (6 bf16
-                MFMA products per fp32 product, fp32-accurate), so peak = the bf16 dense MFMA
-                peak / 6 = 2516.8 / 6 = 419.5 TFLOP/s (MI355X_MICROARCH.md: bf16 = 16 x the
-                157.3 TFLOP/s fp32 MFMA peak, which is reported beside it).  traffic = HBM bytes
+                profiles/ has the rocprofv3 check).  The products are fp32-accurate splits on the
+                16-bit matrix cores: split fp16 (3 MFMAs per fp32 product) in the chains, split
+                bf16 (6) in the dense layers, so peak = the flops-weighted ceiling of that mix,
+                from the fp16/bf16 dense MFMA peak 2516.8 TFLOP/s: /3 = 838.9, /6 = 419.5
+                (MI355X_MICROARCH.md; the 157.3 TFLOP/s fp32 MFMA peak is reported beside it,
+                and frac_vs_split_bf16_ceiling for comparison with earlier rounds).  traffic = HBM bytes
                 per call from rocprofv3 PMC (profiles/pmc_traffic.json, FETCH_SIZE x2 +
                 WRITE_SIZE, per MI355X_MICROARCH.md) when present for this config, else null.
   cpu_baseline  oracle/torch_ref.py -- the reference's formulation in torch-CPU ops -- timed on
@@ -47,6 +49,10 @@ METRIC = "point-clouds/sec forward, SSG B=32 N=1024, at 1/2/4/8 MI355X"
 PEAK_F32_MFMA = 157.3  # TFLOP/s, MI355X_MICROARCH.md chip-level table (dense fp32 MFMA)
 PEAK_BF16_MFMA = 16 * PEAK_F32_MFMA  # TFLOP/s, dense bf16 MFMA (2516.8)
 PEAK_SPLIT = PEAK_BF16_MFMA / 6  # fp32-equivalent ceiling of 6-product split-bf16 MFMA
+# fp32-equivalent ceiling of an MLP call by the planes per operand its kernels ran with
+# (pn2_sa_mlp_last_planes): 3 = split bf16 (6 MFMAs per product), 2 = split fp16 (3; the fp16
+# dense MFMA rate equals bf16's), 1 = bf16 (1), 0 = the fp32 MFMA kernels
+PEAK_BY_PLANES = {3: PEAK_BF16_MFMA / 6, 2: PEAK_BF16_MFMA / 3, 1: PEAK_BF16_MFMA, 0: None}
 PEAK_HBM = 8000.0      # GB/s
 PEAK_F32_VALU = 157.3  # TFLOP/s, MI355X_MICROARCH.md (fp32 vector)
 
@@ -508,13 +514,27 @@ def main():
     roof = None
     if mlp and mlp["ms"] > 0:
         achieved = mlp["flops"] / (mlp["ms"] * 1e-3) / 1e12
-        peak = PEAK_BF16_MFMA if prec == "bf16" else PEAK_SPLIT
+        # the ceiling of the mix the calls ran: sum(flops) / sum(flops_i / peak_i) -- the rate
+        # at which every call at its own arithmetic's MFMA peak would do the same work
+        fbp = {p: f for p, f in mlp["flops_by_planes"].items() if PEAK_BY_PLANES.get(p)}
+        if fbp:
+            peak = sum(fbp.values()) / sum(f / PEAK_BY_PLANES[p] for p, f in fbp.items())
+        else:
+            peak = PEAK_BF16_MFMA if prec == "bf16" else PEAK_SPLIT
+        mix = {{3: "split bf16 x6", 2: "split fp16 x3", 1: "bf16 x1", 0: "fp32"}[p]:
+               round(f / mlp["flops"], 4) for p, f in sorted(mlp["flops_by_planes"].items())}
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1),
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "peak_basis": "flops-weighted MFMA ceiling of the arithmetic each call ran: split "
+                              "fp16 %.1f, split bf16 %.1f, bf16 %.1f TFLOP/s fp32-equivalent" % (
+                                  PEAK_BF16_MFMA / 3, PEAK_BF16_MFMA / 6, PEAK_BF16_MFMA),
+                "flops_mix": mix,
+                "frac_vs_split_bf16_ceiling": round(achieved / PEAK_SPLIT, 4),
                 "traffic": load_traffic(a.config, mlp_name),
                 "compulsory_bytes_per_launch": mlp["bytes"] / mlp["launches"],
                 "kernel": "%s (sa_chain_kernel / dense_split_kernel, %s)" % (
-                    mlp_name, "bf16, 1 MFMA per product" if prec == "bf16" else "split-bf16"),
+                    mlp_name, "bf16, 1 MFMA per product" if prec == "bf16" else
+                    "fp32-accurate split fp16 (chains) / split bf16 (dense layers)"),
                 "fp32_mfma_peak": PEAK_F32_MFMA,
                 "frac_of_fp32_mfma_peak": round(achieved / PEAK_F32_MFMA, 4),
                 "flops_per_launch": mlp["flops"] / mlp["launches"],
@@ -559,7 +579,8 @@ def main():
             "scaling": "strong" if a.config in STRONG else "weak", "vs_baseline": None,
             "dtype": ("bf16 (MLP operands bf16, fp32 accumulate / BN / max; FPS/ball query f32)"
                       if prec == "bf16" else
-                      "f32 (MLP products as 6-term split bf16, fp32 accumulate; FPS/ball query f32)"),
+                      "f32 (MLP products fp32-accurate: split fp16 x3 in the chains, split bf16 x6 in "
+                      "the dense layers, fp32 accumulate; FPS/ball query f32)"),
             "data": "synthetic: seeded uniform clouds normalised to the unit sphere%s; seeded "
                     "random-init weights and BN statistics (eval mode)" % (
                         " + 7-way one-hot" if kind == "onehot10" else ""),

@@ -376,8 +376,8 @@ int pn2_fc_tail_f32(const float *x, int64_t ldx, int64_t B, int64_t K, const flo
 #define PN2_PATH_SPLIT_BF16 2
 #define PN2_PATH_BF16 3
 int pn2_sa_mlp_last_path(void);
-/* Planes per operand of this thread's last register-resident chain launch: 3 (split bf16),
- * 2 (split fp16), 1 (bf16); 0 before any. */
+/* Planes per operand of the MLP kernels of this thread's last successful pn2_sa_mlp_max_* call:
+ * 3 (split bf16: 6 MFMAs per product), 2 (split fp16: 3), 1 (bf16), 0 (fp32 MFMA kernels). */
 int pn2_sa_mlp_last_planes(void);
 
 /* ---- runtime: CU-partitioned streams (pipelined serving, pn2/pipeline.py) ---- */

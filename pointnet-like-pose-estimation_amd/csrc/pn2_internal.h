@@ -86,6 +86,8 @@ constexpr int kMaxC = 16;  // point dims (xyz + one-hot) held in registers
 int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
                      float *out, int64_t ostride, int64_t M, int64_t K, int np, float *ws,
                      int64_t ws_bytes, hipStream_t st);
+// planes per operand of this thread's last chain launch (3 split bf16, 2 split fp16, 1 bf16)
+int chain_last_planes();
 // sa_dense.hip: split-bf16 layer-by-layer path for group_all / dense-row chains
 int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np);
 int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,

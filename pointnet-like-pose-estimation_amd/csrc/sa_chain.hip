@@ -1446,4 +1446,4 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
 
 }  // namespace pn2
 
-extern "C" int pn2_sa_mlp_last_planes(void) { return pn2::g_last_planes; }
+int pn2::chain_last_planes() { return pn2::g_last_planes; }

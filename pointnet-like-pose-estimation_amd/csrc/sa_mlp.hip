@@ -866,7 +866,9 @@ static int run_plan(const pn2_sa_src &cur, const pn2_mlp_layer *layers, int l0, 
 }
 
 static thread_local int g_last_path = 0;
+static thread_local int g_last_planes = 0;  // planes per operand of the call's MLP kernels
 extern "C" int pn2_sa_mlp_last_path(void) { return g_last_path; }
+extern "C" int pn2_sa_mlp_last_planes(void) { return g_last_planes; }
 
 // the src's zero side job on the paths whose kernels do not take it (the dense-layer path's
 // last layer does)
@@ -890,13 +892,13 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
     rc = try_launch_chain(*src, layers, nlayers, pool, out, ostride, M, K, 3, workspace,
                           workspace_bytes, st);
     if (rc != 0) {
-        if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
+        if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16, g_last_planes = chain_last_planes();
         return rc < 0 ? rc : zero_side_job(*src, st);
     }
     rc = try_launch_dense_split(*src, layers, nlayers, pool, out, ostride, workspace, workspace_bytes,
                                 M, K, 3, st);
     if (rc != 0) {
-        if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16;
+        if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16, g_last_planes = 3;
         return rc < 0 ? rc : PN2_OK;
     }
     if ((rc = zero_side_job(*src, st)) != PN2_OK) return rc;
@@ -905,6 +907,7 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
             return set_error(PN2_EUNSUPPORTED, "pn2_sa_mlp_max_f32: layer %d without ReLU needs the split "
                              "dense-layer path (group_all / rows source, split weight images)", l);
     g_last_path = PN2_PATH_F32;
+    g_last_planes = 0;
     const int64_t w = workspace_width(*src, layers, nlayers, M, K);
     if (w > 0)
         PN2_REQUIRE(workspace && workspace_bytes >= 2 * M * w * 4 && ((uintptr_t)workspace & 15) == 0,
@@ -973,5 +976,6 @@ extern "C" int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *l
                          "pn2_sa_mlp_max_bf16: no bf16 kernel for this chain (%d layers, mode %d) "
                          "or workspace too small", nlayers, src->mode);
     g_last_path = PN2_PATH_BF16;
+    g_last_planes = 1;
     return PN2_OK;
 }

@@ -56,20 +56,26 @@ def mlp_precision(precision: str):
 
 class KernelTimer:
     """HIP-event timing of every libpn2 launch, recorded on the stream the launch is issued on
-    (torch's current stream), with each launch's algorithmic FLOPs / bytes."""
+    (torch's current stream), with each launch's algorithmic FLOPs / bytes and, for the MLP
+    calls, the planes per operand its kernels ran with (pn2_sa_mlp_last_planes)."""
 
     def __init__(self):
-        self.records = []  # (name, start_event, end_event, flops, bytes)
+        self.records = []  # (name, start_event, end_event, flops, bytes[, planes])
 
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, e0, e1, flops, nbytes in self.records:
-            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+        for rec in self.records:
+            name, e0, e1, flops, nbytes = rec[:5]
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0,
+                                      "flops_by_planes": {}})
             d["launches"] += 1
             d["ms"] += e0.elapsed_time(e1)
             d["flops"] += flops
             d["bytes"] += nbytes
+            if len(rec) > 5:
+                fp = d["flops_by_planes"]
+                fp[rec[5]] = fp.get(rec[5], 0.0) + flops
         return out
 
 
@@ -469,6 +475,8 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
          (src, layers, n, 1 if pool else 0, out.data_ptr(), out.stride(-2),
           0 if ws is None else ws.data_ptr(), ws_bytes, _stream(dev_t)), dev_t.device, flops=flops,
          nbytes=nbytes)
+    if _TIMER is not None and _TIMER.records and _TIMER.records[-1][0] == name:
+        _TIMER.records[-1] = _TIMER.records[-1] + (int(_L.pn2_sa_mlp_last_planes()),)
 
 
 sa_mlp_max_ = torch.library.custom_op("pn2::sa_mlp_max_", sa_mlp_max_direct, mutates_args=("out", "zero"))

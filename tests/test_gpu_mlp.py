@@ -302,7 +302,9 @@ F16 = [
     (3, 0, 32, 64, 512, 0.2, [64, 64, 128], False, "tiny_row"),     # one weight row 1e-6, var 1e-12
     (3, 0, 32, 64, 512, 0.2, [64, 64, 128], False, "hidden_1e4"),   # layer-1 inputs ~1e4
     (3, 0, 32, 64, 512, 0.2, [64, 64, 128], False, "hidden_1e-5"),  # layer-1 inputs ~1e-5
-    (3, 16, 16, 64, 512, 0.3, [32, 32, 64], True, "plain"),         # MSG row order, pre-pass
+    (3, 0, 16, 64, 512, 0.3, [32, 32, 64], True, "plain"),          # MSG row order (xyz only)
+    (3, 96, 32, 32, 256, 0.35, [64, 64, 128], True, "plain"),       # MSG, wide layer 0 -> pre-pass
+    (3, 16, 16, 64, 512, 0.3, [32, 32, 64], True, "streamed"),      # streamed layer 0: split bf16
 ]
 
 
@@ -351,7 +353,7 @@ def test_chain_split_f16_vs_oracle(case, f16):
             newp, newf = sa(x.to(DEV), None if f is None else f.to(DEV))
         torch.cuda.synchronize()
     assert _lib.load().pn2_sa_mlp_last_path() == _lib.PATH_SPLIT_BF16
-    assert _lib.load().pn2_sa_mlp_last_planes() == (2 if f16 else 3)
+    assert _lib.load().pn2_sa_mlp_last_planes() == (2 if f16 and kind != "streamed" else 3)
     ps = x.permute(0, 2, 1)
     torch.manual_seed(900 + case)
     start = torch.randint(0, N, (B,), dtype=torch.long)
