@@ -596,6 +596,8 @@ def main():
                            " on %d dedicated CUs" % a.geometry_cus if a.geometry_cus > 0
                            else "s sharing all CUs") + (
                            "; geometry of %d batches per replay" % a.geometry_batches +
+                           ("; one forward per geometry group" if getattr(pf, "_slots", None) and
+                            pf._slots[0].halves[0].fused else "; one forward per batch") +
                            ("; %d compute + %d geometry streams%s" % (
                                pf.compute_streams, pf.geometry_streams,
                                "" if pf.head_on_tail else ", heads on the compute streams"))

@@ -1321,7 +1321,11 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     // the fp32-accurate chains run split fp16 (3 MFMAs per product, split_bf16.h) where a whole
     // layer-0 input is in registers or pre-transformed (the activation scale needs the wave's
     // whole input); tuning chain_f16 = 0 keeps split bf16 (6 MFMAs)
-    const int npk = (np == 3 && tuning().chain_f16 && (KB0M == 1 || KB0M == -1)) ? 2 : np;
+    // The activation scale is per wave (32 rows): a cloud's rows must start at a wave boundary
+    // (compact launches: a workgroup per cloud; else S*K a multiple of 32), so a cloud's results
+    // never depend on which other clouds share its batch.
+    const bool f16_ok = compact || (s.S * K) % 32 == 0;
+    const int npk = (np == 3 && tuning().chain_f16 && f16_ok && (KB0M == 1 || KB0M == -1)) ? 2 : np;
     const size_t stage_b = npk == 3 ? stage_bytes<3>() : npk == 2 ? stage_bytes<2>() : stage_bytes<1>();
     const int wpc = compact ? (int)compact_wpc(s) : 0;
     // Compact launches: the weight ring's depth against the LDS group pool.  With the full

@@ -370,6 +370,15 @@ def _clone(o):
     return o
 
 
+def _rows(o, lo, hi):
+    """Rows [lo, hi) (dim 0) of every tensor of a (nested) output: batch h of a fused group's."""
+    if isinstance(o, torch.Tensor):
+        return o[lo:hi]
+    if isinstance(o, (tuple, list)):
+        return type(o)(_rows(t, lo, hi) for t in o)
+    return o
+
+
 def _flat_tensors(o):
     if isinstance(o, torch.Tensor):
         return [o]
@@ -384,7 +393,13 @@ _MODE = "thread_local"
 
 
 class _Slot:
-    """Static buffers and graphs of one batch slot: one batch of a geometry group."""
+    """Static buffers and graphs of one batch slot: one batch of a geometry group, or the whole
+    group (``fused``)."""
+    fused = False
+
+
+class _Restart(Exception):
+    """An SA module was replaced between runs: the geometry graphs are stale (run() restarts)."""
 
 
 class _Group:
@@ -462,8 +477,14 @@ class GraphedPipeline(PipelinedForward):
     """
 
     def __init__(self, model, geometry_cus=0, tail=True, nslots=8, geometry_streams=1,
-                 geometry_batches=2, compute_streams=None):
+                 geometry_batches=2, compute_streams=None, fuse=None):
         super().__init__(model, geometry_cus, bool(tail))
+        # fuse: one forward (sa + head graphs) over the whole geometry group -- its gb batches
+        # side by side, every launch with gb times the rows -- instead of one per batch.  Each
+        # cloud is computed exactly as in its own batch's forward (per-cloud kernels; the FC
+        # tail computes a row the same way at any row count), so the outputs are the per-batch
+        # ones, sliced.  Default: tuning pipe_fuse.
+        self.fuse = bool(tuning.get("pipe_fuse")) if fuse is None else bool(fuse)
         gb = int(geometry_batches)
         if gb < 1:
             raise ValueError("pn2.pipeline: geometry_batches must be >= 1")
@@ -557,9 +578,22 @@ class GraphedPipeline(PipelinedForward):
         torch.cuda.synchronize(dev)
         grp.entries = entries
         grp.B = B
-        grp.halves = [self._capture_forward(xs[h], extra, dev, *self._half_entries(grp, h))
-                      for h in range(gb)]
+        grp.halves = self._group_forwards(grp, xs, extra, dev)
         return grp
+
+    def _group_forwards(self, grp, xs, extra, dev):
+        """The group's forward graphs: one per batch, or (fuse) one over the whole group."""
+        gb = self.gb
+        if self.fuse and gb > 1:
+            ex = [torch.cat([e] * gb) for e in extra]
+            sl = self._capture_forward(grp.x, ex, dev, *self._half_entries(grp, None))
+            outs = _flat_tensors(sl.out)
+            if outs and all(t.dim() >= 1 and t.shape[0] == gb * grp.B for t in outs):
+                sl.fused = True
+                return [sl]
+            # an output without the batch as its first dimension: per-batch forwards
+        return [self._capture_forward(xs[h], extra, dev, *self._half_entries(grp, h))
+                for h in range(gb)]
 
     def _half_entries(self, grp, h):
         """Batch h's slice of the group's geometry, keyed by the tensor its SA module is called
@@ -570,8 +604,8 @@ class GraphedPipeline(PipelinedForward):
         for _, newp, _, _, _ in grp.entries.values():
             srcs[newp.data_ptr()] = newp
 
-        def part(t):
-            return t[h * B:(h + 1) * B]
+        def part(t):  # h None: the whole group (a fused forward)
+            return t if h is None else t[h * B:(h + 1) * B]
 
         geo = set()
         for _, newp, cpk, ppk, idxs in grp.entries.values():
@@ -588,8 +622,9 @@ class GraphedPipeline(PipelinedForward):
         are kept."""
         with tuning.pipeline_profile():
             for grp in self._slots:
-                grp.halves = [self._capture_forward(sl.x, extra, dev, *self._half_entries(grp, h))
-                              for h, sl in enumerate(grp.halves)]
+                B = grp.B
+                grp.halves = self._group_forwards(
+                    grp, [grp.x[h * B:(h + 1) * B] for h in range(self.gb)], extra, dev)
 
     def _capture_forward(self, x, extra, dev, entries, geo):
         sl = _Slot()
@@ -730,8 +765,8 @@ class GraphedPipeline(PipelinedForward):
                 ev_read[s] = []
                 mark(js[0] - first, "geo0", geo)
                 for h, j in enumerate(js):
-                    grp.halves[h].x.copy_(batches[j if j < len(batches) else js[0]],
-                                          non_blocking=True)
+                    grp.x[h * grp.B:(h + 1) * grp.B].copy_(batches[j if j < len(batches) else js[0]],
+                                                           non_blocking=True)
                 grp.start_buf.copy_(self._draw_row(starts, g, nh), non_blocking=True)
                 grp.fps.replay()
                 ev_fps[s] = geo.record_event()
@@ -753,6 +788,22 @@ class GraphedPipeline(PipelinedForward):
                 issue_fps(issued[0])
                 issued[0] += 1
 
+        if self._slots[0].halves[0].fused:
+            try:
+                with torch.no_grad():
+                    self._run_fused(batches, extra_of, post, first, outs, ngr, geos, mains, tails,
+                                    tail, ev_fps, ev_read, ev_head, top_up, check_params, dev, mark)
+            except _Restart:
+                torch.cuda.synchronize(dev)
+                shard.set_rng_state(rng0)
+                self._slots = None
+                return self.run(batches, extras, post)
+            for g in geos[1:]:
+                geo.wait_stream(g)
+            self._pinned_evs[self._pinned_cur] = geo.record_event()  # uploads read it
+            for st in [geo] + mains + tails:
+                caller.wait_stream(st)
+            return outs
         with torch.no_grad():
             # the geometry runs up to ng-1 groups ahead of the compute streams
             for i in range(first, len(batches)):
@@ -825,6 +876,65 @@ class GraphedPipeline(PipelinedForward):
         for st in [geo] + mains + tails:
             caller.wait_stream(st)
         return outs
+
+    def _run_fused(self, batches, extra_of, post, first, outs, ngr, geos, mains, tails, tail,
+                   ev_fps, ev_read, ev_head, top_up, check_params, dev, mark):
+        """run()'s issue loop with fused group forwards: per geometry group one sa graph (on
+        the compute streams in turn) and one head graph (tail stream) over its gb batches; the
+        outputs are split into per-batch rows, `post` runs per batch in batch order."""
+        gb, ng = self.gb, self.ngroups
+        drain = int(tuning.get("drain_heads"))
+        drain_groups = (drain + gb - 1) // gb
+        for g in range(ngr):
+            s = g % ng
+            i0 = first + g * gb
+            js = [i0 + h for h in range(gb) if i0 + h < len(batches)]
+            top_up(g, -1)
+            if check_params:  # (first group: its geometry is issued)
+                check_params = False
+                if self._params.key() != self._pkey:
+                    if [id(m) for m in self._find_sas()] != [id(m) for m in self.sas]:
+                        raise _Restart()
+                    self._recapture_forwards(extra_of(i0), dev)
+                    self._pkey = self._params.key()
+            grp = self._slots[s]
+            sl = grp.halves[0]
+            B = grp.B
+            main = mains[g % len(mains)]
+            with torch.cuda.stream(main):
+                main.wait_event(ev_fps[s])
+                if ev_head[s] is not None:  # the slot's last head is done with the pool
+                    main.wait_event(ev_head[s])
+                for h in range(gb):
+                    for d, e in zip(sl.extra, extra_of(js[h] if h < len(js) else js[0])):
+                        d[h * B:(h + 1) * B].copy_(e, non_blocking=True)
+                mark(i0 - first, "sa0", main)
+                sl.sa.replay()
+                ev_sa = main.record_event()
+                mark(i0 - first, "sa1", main)
+            ts = tails[g % len(tails)] if (sl.head is not None and self.head_on_tail and
+                                           g < ngr - drain_groups) else main
+            with torch.cuda.stream(ts):
+                if sl.head is not None:
+                    if ts is not main:
+                        ts.wait_event(ev_sa)
+                    mark(i0 - first, "hd0", ts)
+                    sl.head.replay()
+                full = _clone(sl.out)
+                ev_read[s].append(ts.record_event() if sl.tail_reads_geometry else ev_sa)
+                outs_g = [_rows(full, h * B, (h + 1) * B) for h in range(len(js))]
+                if post is not None and ts is tail:
+                    outs_g = [post(j, o) for j, o in zip(js, outs_g)]
+                ev_head[s] = ts.record_event()
+                mark(i0 - first, "hd1", ts)
+            if post is not None and ts is not tail:
+                tail.wait_stream(ts)
+                with torch.cuda.stream(tail):
+                    for t in _flat_tensors(full):
+                        t.record_stream(tail)
+                    outs_g = [post(j, o) for j, o in zip(js, outs_g)]
+            outs.extend(outs_g)
+            top_up(-1, g + ng)
 
     def _draw_all(self, k):
         """The pinned host buffer that receives the start draws of the next k groups, one row

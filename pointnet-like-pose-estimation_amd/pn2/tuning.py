@@ -24,6 +24,8 @@ Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_s
                      bench's --force-rccl measurement of the collective's cost on one GPU)
     geometry_bq      1: the pipeline's geometry stream runs the ball queries after the FPS;
                      0: only the FPS, each batch's forward (compute stream) queries
+    pipe_fuse        1: GraphedPipeline runs one forward (sa + head graphs) per geometry group,
+                     its batches side by side; 0: one forward per batch
     pipe_profile     1: the pipelines (pn2.pipeline) capture and run their kernels under
                      PIPELINE_PROFILE -- the launch choices measured best beside each other's
                      kernels, where the kernel defaults are the ones measured best alone (the
@@ -49,6 +51,7 @@ HOST_DEFAULTS = {
     "force_gather": 0,
     "tail_streams": 1,
     "geometry_bq": 1,
+    "pipe_fuse": 1,
 }
 
 

@@ -62,7 +62,7 @@ def main():
             gp.run([x] * 12)  # captures the graphs with the stand-ins
             ops.fps_direct, ops.ball_query_direct = real_fps, real_bq
     torch.cuda.synchronize()
-    K = 100
+    K = int(os.environ.get("K", "100"))
     for rnd in range(3):
         for k, gp in gps.items():
             torch.cuda.synchronize()
@@ -70,7 +70,7 @@ def main():
             with torch.no_grad():
                 gp.run([x] * K)
             torch.cuda.synchronize()
-            print("round %d %-7s %8.0f clouds/s" % (rnd, k, 32 * K / (time.perf_counter() - t0)))
+            print("round %d %-7s K=%d %8.0f clouds/s" % (rnd, k, K, 32 * K / (time.perf_counter() - t0)))
 
 
 if __name__ == "__main__":
