@@ -1354,8 +1354,13 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
         if (wgs(2, 8) > wgs(2, kUnitsPerWG)) cprow = 8;
         if (tuning().compact_pool > 0)
             cprow = (int)std::max<int64_t>(1, std::min<int64_t>(kUnitsPerWG, tuning().compact_pool));
-        if (tuning().compact_stages == 3 && wgs(3, 8) >= wgs(2, kUnitsPerWG))
-            cks = 3, cprow = 8;
+        // the 3-stage ring where it keeps the workgroups per CU: with the whole pool when that
+        // fits too (split-fp16 rings are a third smaller: SSG sa2 then needs no HBM merges),
+        // else with the 8-row pool
+        if (tuning().compact_stages == 3) {
+            if (wgs(3, cprow) >= wgs(2, kUnitsPerWG)) cks = 3;
+            else if (wgs(3, 8) >= wgs(2, kUnitsPerWG)) cks = 3, cprow = 8;
+        }
     }
     int *cunits = nullptr;
     int2 *cdesc = nullptr;

@@ -271,3 +271,30 @@ def test_linear_rows_matches_torch(B, K, N, relu):
     got = ops.linear_rows(xs, W, None, False)
     ref = xs.double() @ W.double().t()
     assert_close(got.cpu().numpy(), ref.cpu().numpy(), 2e-6)
+
+
+@pytest.mark.gpu
+def test_v1_pointnet_cls_at_config_batch():
+    """BASELINE config 1 runs pointnet_cls at B = 8; the v1 dense kernels pick their tile widths
+    by row count, so the B = 8 launch is checked too: the golden's 4 clouds twice over (the
+    second copy reversed) must each give the reference's per-cloud outputs, and equal copies
+    the same bits."""
+    g = load_golden("v1_pointnet_cls.npz")
+    model, _ = _build("pointnet_cls")
+    model = model.to("cuda").eval()
+    x4 = torch.from_numpy(g["input"])
+    B0 = x4.shape[0]
+    order = list(range(B0)) + list(reversed(range(B0)))
+    x8 = x4[order].contiguous().to("cuda")
+    with torch.no_grad():
+        out = model(x8)
+    outs = out if isinstance(out, tuple) else (out,)
+    for i, o in enumerate(outs):
+        o = o.detach().cpu().numpy()
+        want = g["out%d" % i][order]
+        if o.dtype == np.int64:
+            np.testing.assert_array_equal(o, want)
+        else:
+            assert_close(o, want, 1e-4)
+        for k in range(B0):  # cloud k in both copies: identical bits
+            np.testing.assert_array_equal(o[k], o[2 * B0 - 1 - k])
