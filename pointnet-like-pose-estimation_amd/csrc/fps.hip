@@ -507,10 +507,7 @@ static int launch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t
     constexpr int SLOT = (CM + 2 + 3) & ~3;
     const size_t head = (size_t)((S + 3) & ~3) * 4 + 32;
     const size_t cloud = (size_t)N * (CM == 3 ? 4 : CM) * 4;
-    // tuning fps_slots = 1: the winner's coordinates travel with the per-wave slots instead of
-    // being read from an LDS copy of the cloud after the key (A/B)
-    const bool ldsc = CR == CM && cloud <= (size_t)kFpsLdsCloud && head + cloud <= (size_t)160 * 1024 &&
-                      !tuning().fps_slots;
+    const bool ldsc = CR == CM && cloud <= (size_t)kFpsLdsCloud && head + cloud <= (size_t)160 * 1024;
     const size_t lds = head + (ldsc ? cloud : (size_t)2 * NW * SLOT * 4);
     if constexpr (CR != CM) {
         hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, false, CR>), dim3((unsigned)B), dim3(NT), lds, st,

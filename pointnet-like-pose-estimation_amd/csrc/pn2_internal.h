@@ -47,7 +47,6 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
                            /* are written straight to HBM (0: always)                      */ \
     X(fps_threads, 0)      /* FPS block shape threads x points per thread (0: automatic)   */ \
     X(fps_ppt, 0)                                                                              \
-    X(fps_slots, 0)        /* 1: FPS winner coordinates through per-wave slots (no cloud copy) */ \
     X(fps_mid, 512)        /* automatic FPS block for 256 < N <= 1024: 512 threads x 2      */ \
                            /* points (fastest alone: the eager forward) or 256 x 4 (the     */ \
                            /* pipelines' geometry, beside the chains)                       */ \

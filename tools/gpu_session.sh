@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box runner for one A/B iteration:
-#   PYTEST="-k expr" (optional: GPU tests first; "all" = the whole -m gpu suite)
+#   PYTEST=all (optional: the whole -m gpu suite first) or PYTEST_K="expr" (a -k selection)
 #   KT="tag:tuning|tag:tuning" (optional: eager rocprofv3 kernel traces per PN2_TUNING variant,
 #                                summarised by tools/kstats.py)
 #   VARIANTS=... (optional: interleaved bench A/B, tools/args_ab.sh syntax), STEPS, WARMUP, ROUNDS
@@ -11,8 +11,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/sess
 mkdir -p $OUT
 export TMPDIR=/tmp
-if [ -n "${PYTEST:-}" ]; then
-  if [ "$PYTEST" = all ]; then sel=(); else sel=($PYTEST); fi
+if [ -n "${PYTEST:-}" ] || [ -n "${PYTEST_K:-}" ]; then
+  if [ -n "${PYTEST_K:-}" ]; then sel=(-k "$PYTEST_K"); else sel=(); fi
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${sel[@]}" > $OUT/pytest.log 2>&1
   rc=$?; tail -4 $OUT/pytest.log; [ $rc -ne 0 ] && { echo "pytest rc=$rc"; exit $rc; }
 fi
