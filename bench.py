@@ -98,15 +98,17 @@ def parse():
                     help="eager pipeline: run the head on its own stream (default off there)")
     ap.add_argument("--no-tail", action="store_true",
                     help="graphed pipeline: keep the head on the compute stream")
-    ap.add_argument("--slots", type=int, default=8,
+    ap.add_argument("--slots", type=int, default=None,
                     help="graphed pipeline: batch slots (a multiple of --geometry-batches; the "
-                         "geometry runs slots/geometry-batches - 1 groups ahead)")
+                         "geometry runs slots/geometry-batches - 1 groups ahead; default 4 "
+                         "groups)")
     ap.add_argument("--compute-streams", type=int, default=None,
                     help="graphed pipeline: consecutive batches' forwards alternate between this "
                          "many compute streams (1 or 2; default 2 with shared CUs)")
-    ap.add_argument("--geometry-batches", type=int, default=2,
+    ap.add_argument("--geometry-batches", type=int, default=4,
                     help="graphed pipeline: consecutive batches whose geometry (FPS + ball "
-                         "queries) runs as one replay over their clouds side by side")
+                         "queries) runs as one replay over their clouds side by side, and (tuning "
+                         "pipe_fuse) whose forward runs as one")
     ap.add_argument("--geometry-streams", type=int, default=None,
                     help="graphed pipeline: 2 = consecutive groups' FPS chains on two streams "
                          "(default 2 for --config stress, else 1)")
@@ -414,7 +416,8 @@ def main():
             eager_models, [i for i, n in enumerate(names) if n.startswith("translation")])
         if not a.eager_pipeline:
             pf = GraphedPipeline(pmodel, geometry_cus=a.geometry_cus,
-                                 tail=not a.no_tail, nslots=a.slots,
+                                 tail=not a.no_tail,
+                                 nslots=a.slots if a.slots is not None else 4 * a.geometry_batches,
                                  geometry_streams=(a.geometry_streams if a.geometry_streams is not None
                                                    else DEFAULT_GEOMETRY_STREAMS.get(a.config, 1)),
                                  geometry_batches=a.geometry_batches,

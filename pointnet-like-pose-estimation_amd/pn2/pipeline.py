@@ -476,8 +476,8 @@ class GraphedPipeline(PipelinedForward):
     91 / 106k (unexplained; reproducible per count).
     """
 
-    def __init__(self, model, geometry_cus=0, tail=True, nslots=8, geometry_streams=1,
-                 geometry_batches=2, compute_streams=None, fuse=None):
+    def __init__(self, model, geometry_cus=0, tail=True, nslots=16, geometry_streams=1,
+                 geometry_batches=4, compute_streams=None, fuse=None):
         super().__init__(model, geometry_cus, bool(tail))
         # fuse: one forward (sa + head graphs) over the whole geometry group -- its gb batches
         # side by side, every launch with gb times the rows -- instead of one per batch.  Each
