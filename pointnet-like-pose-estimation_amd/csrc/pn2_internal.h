@@ -36,6 +36,7 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
 #define PN2_TUNING_KEYS(X)                                                                     \
     X(mlp_f32, 0)          /* 1: fp32 MFMA kernels instead of the split-bf16 ones          */ \
     X(chain_f16, 1)        /* 1: fp32-accurate chains as split fp16 (3 MFMAs per product)   */ \
+    X(dense_f16, 1)        /* 1: fp32-accurate dense layers after the first as split fp16   */ \
                            /* where eligible; 0: split bf16 (6)                             */ \
     X(chain_prepass, 1)    /* 0: no layer-0 pre-pass (wide first layers of a chain)        */ \
     X(compact, 1)          /* 0: no compact neighbourhoods (every padded row computed)     */ \
@@ -90,6 +91,9 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
 int chain_last_planes();
 // sa_dense.hip: split-bf16 layer-by-layer path for group_all / dense-row chains
 int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np);
+int64_t dense_split_ws_bytes(int64_t M, int64_t w);
+// planes per operand carrying most of the flops of the calling thread's last dense-layer call
+int dense_last_planes();
 int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
                            float *out, int64_t ostride, float *ws, int64_t ws_bytes, int64_t M,
                            int64_t K, int np, hipStream_t st);

@@ -967,15 +967,6 @@ extern "C" int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin, int64_t xyz)
     return 5 * cout * kbs * 16 * 2 + (cout * 4 + 15) / 16 * 16;
 }
 
-namespace pn2 {
-// the NP = 2 planes and the row scales inside a pn2_pack_layer_split_bf16 image
-static const bf16x8 *split_f16_planes(const void *img, int64_t cout, int64_t kbs) {
-    return reinterpret_cast<const bf16x8 *>(static_cast<const char *>(img) + 3 * cout * kbs * 32);
-}
-static const float *split_f16_inv_scale(const void *img, int64_t cout, int64_t kbs) {
-    return reinterpret_cast<const float *>(static_cast<const char *>(img) + 5 * cout * kbs * 32);
-}
-}  // namespace pn2
 
 extern "C" int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t xyz,
                                          int xyz_first, void *out, void *stream) {

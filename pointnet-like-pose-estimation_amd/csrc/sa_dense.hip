@@ -87,7 +87,49 @@ struct DenseSplitArgs {
     // dense_lds_kernel: XCD x runs a (row blocks / (8 / xcx)) x (column tiles / xcx) rectangle of
     // the output (0: XCD-contiguous logical ids, whole row blocks per XCD)
     int xcx;
+    // split fp16 (NP = 2, rows mode): w = the image's fp16 planes, wscale the weight rows' inverse
+    // scales, in_max [M/32][in_tiles] the producing layer's per-(32-row block, 32-column tile)
+    // max |value| bits (split_bf16.h): each wave's activation scale
+    const float *wscale;
+    const unsigned *in_max;
+    int in_tiles;
+    // out_max [M/32][tiles] (or null): this layer's own per-(row block, tile) max |value| bits of
+    // the rows it writes (pool == 0), for an NP = 2 layer after it
+    unsigned *out_max;
 };
+
+// NP = 2: this wave's activation scale (rows rb*32 .. rb*32+31 of a rows-mode input)
+template <int NP>
+__device__ __forceinline__ ActScale dense_act_scale(const DenseSplitArgs &A, int rb, int lane) {
+    if constexpr (NP != 2) {
+        return ActScale{1.f, 1.f};
+    } else {
+        unsigned m = 0;
+        if (32 * rb < A.M)
+            for (int t = lane; t < A.in_tiles; t += 64) m = max(m, A.in_max[(int64_t)rb * A.in_tiles + t]);
+        return act_scale(__uint_as_float(wave_max_u32(m)));
+    }
+}
+// a k-block of the A operand split, scaled first for NP = 2
+template <int NP>
+__device__ __forceinline__ Split split_scaled(const float (&x)[8], float up) {
+    if constexpr (NP == 2) {
+        float y[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = x[j] * up;
+        return splitN<NP>(y);
+    } else {
+        return splitN<NP>(x);
+    }
+}
+// the BN scale of output column col (NP = 2: times the weight row's inverse scale and the
+// wave's activation down-scale)
+template <int NP>
+__device__ __forceinline__ float dense_alpha(const DenseSplitArgs &A, int col, float down) {
+    if (A.raw) return 1.f;
+    if constexpr (NP == 2) return A.alpha[col] * A.wscale[col] * down;
+    else return A.alpha[col];
+}
 
 // Signed max through unsigned atomics: key() is monotone from float order to uint order (and
 // key(anything) > 0, so a zeroed pool is below every value); unkey() inverts it.
@@ -156,6 +198,7 @@ void dense_split_kernel(const DenseSplitArgs A) {
     // ---- this lane's row (A operand)
     const int R = row0 + 32 * wave + r;
     const bool valid = R < A.M;
+    const ActScale asc = dense_act_scale<NP>(A, (row0 >> 5) + wave, lane);
     const float *arow = nullptr, *frow = nullptr, *prow = nullptr;
     if (A.mode == 0) {
         arow = A.rows + (int64_t)(valid ? R : 0) * A.rs;
@@ -287,7 +330,7 @@ void dense_split_kernel(const DenseSplitArgs A) {
             // (sched_group_barrier) measured no faster, and cost registers.
 #pragma unroll
             for (int k = 0; k < kKC; ++k) {
-                const Split xs = splitN<NP>(xc[k]);
+                const Split xs = split_scaled<NP>(xc[k], asc.up);
 #pragma unroll
                 for (int i = 0; i < NTC; ++i)
                     acc[i] = mma_wb<NP>(xs, ring_readN<NP>(buf + (k * kFrag + NP * i) * 1024, lane), acc[i]);
@@ -296,7 +339,7 @@ void dense_split_kernel(const DenseSplitArgs A) {
 #pragma unroll
             for (int k = 0; k < kKC; ++k) {
                 if (c * kKC + k < A.kb) {
-                    const Split xs = splitN<NP>(xc[k]);
+                    const Split xs = split_scaled<NP>(xc[k], asc.up);
 #pragma unroll
                     for (int i = 0; i < NTC; ++i)
                         acc[i] = mma_wb<NP>(xs, ring_readN<NP>(buf + (k * kFrag + NP * i) * 1024, lane), acc[i]);
@@ -320,15 +363,22 @@ void dense_split_kernel(const DenseSplitArgs A) {
 #pragma unroll
     for (int i = 0; i < NTC; ++i) {
         const int col = 32 * (ct0 + i) + r;
-        const float al = A.raw ? 1.f : A.alpha[col], be = A.raw ? 0.f : A.beta[col];
+        const float al = dense_alpha<NP>(A, col, asc.down), be = A.raw ? 0.f : A.beta[col];
         if (!A.pool) {
+            unsigned tmax = 0;  // max |value| written (A.out_max)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int row = slab_row + (q & 3) + 8 * (q >> 2) + 4 * h;
                 if (row < A.M) {
                     const float y = __builtin_fmaf(acc[i][q], al, be);
-                    A.out[(int64_t)row * A.ostride + col] = A.raw ? acc[i][q] : (A.norelu ? y : chain_relu(y));
+                    const float v = A.raw ? acc[i][q] : (A.norelu ? y : chain_relu(y));
+                    A.out[(int64_t)row * A.ostride + col] = v;
+                    tmax = max(tmax, __float_as_uint(v) & 0x7FFFFFFFu);
                 }
+            }
+            if (A.out_max) {
+                const unsigned m = wave_max_u32(tmax);
+                if (lane == 0 && slab_row < A.M) A.out_max[(int64_t)(slab_row >> 5) * A.tiles + ct0 + i] = m;
             }
             continue;
         }
@@ -553,6 +603,7 @@ void dense_lds_kernel(const DenseSplitArgs A) {
     for (int s = 0; s < NS - 1; ++s)
         if (s < nst) issue(s);
     const int trow = 32 * wave + r;  // this lane's tile row (A fragment)
+    const ActScale asc = dense_act_scale<NP>(A, (row0 >> 5) + wave, lane);
     if (A.mode == 1) {
         // block 0: raw xyz of the point (sample_and_group_all does not centre), and its
         // fragments straight from L2
@@ -583,7 +634,7 @@ void dense_lds_kernel(const DenseSplitArgs A) {
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
         const int col = 32 * (ct0 + i) + r;
-        eal[i] = A.raw ? 1.f : A.alpha[col];
+        eal[i] = dense_alpha<NP>(A, col, asc.down);
         ebe[i] = A.raw ? 0.f : A.beta[col];
     }
     // ---- main loop, software-pipelined across stages.  Without it both waves of a SIMD left
@@ -629,7 +680,7 @@ void dense_lds_kernel(const DenseSplitArgs A) {
             float x[8];
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[i] = f.a[kbl][0][i], x[4 + i] = f.a[kbl][1][i];
-            xs[kbl] = splitN<NP>(x);
+            xs[kbl] = split_scaled<NP>(x, asc.up);
         }
     };
     auto mfma_kb = [&](const Split &xs, const Frags &f, int kbl) {
@@ -692,13 +743,20 @@ void dense_lds_kernel(const DenseSplitArgs A) {
         const int col = 32 * ct0 + lcol;
         const float al = eal[i], be = ebe[i];
         if (!A.pool) {
+            unsigned tmax = 0;  // max |value| written (A.out_max)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int row = slab_row + (q & 3) + 8 * (q >> 2) + 4 * h;
                 if (row < A.M) {
                     const float y = __builtin_fmaf(acc[i][q], al, be);
-                    A.out[(int64_t)row * A.ostride + col] = A.raw ? acc[i][q] : (A.norelu ? y : chain_relu(y));
+                    const float v = A.raw ? acc[i][q] : (A.norelu ? y : chain_relu(y));
+                    A.out[(int64_t)row * A.ostride + col] = v;
+                    tmax = max(tmax, __float_as_uint(v) & 0x7FFFFFFFu);
                 }
+            }
+            if (A.out_max) {
+                const unsigned m = wave_max_u32(tmax);
+                if (lane == 0 && slab_row < A.M) A.out_max[(int64_t)(slab_row >> 5) * A.tiles + ct0 + i] = m;
             }
             continue;
         }
@@ -804,12 +862,16 @@ static int launch_dense_lds(const DenseSplitArgs &A, hipStream_t st) {
 }
 
 static int launch_dense_lds_tile(int tile, const DenseSplitArgs &A, int np, hipStream_t st) {
+#define PN2_LDS_NP(WR, NTW) \
+    (np == 3 ? launch_dense_lds<WR, NTW, 3>(A, st) : np == 2 ? launch_dense_lds<WR, NTW, 2>(A, st) \
+             : launch_dense_lds<WR, NTW, 1>(A, st))
     switch (tile) {
-        case 82: return np == 3 ? launch_dense_lds<8, 2, 3>(A, st) : launch_dense_lds<8, 2, 1>(A, st);
-        case 44: return np == 3 ? launch_dense_lds<4, 4, 3>(A, st) : launch_dense_lds<4, 4, 1>(A, st);
-        case 42: return np == 3 ? launch_dense_lds<4, 2, 3>(A, st) : launch_dense_lds<4, 2, 1>(A, st);
-        default: return np == 3 ? launch_dense_lds<2, 2, 3>(A, st) : launch_dense_lds<2, 2, 1>(A, st);
+        case 82: return PN2_LDS_NP(8, 2);
+        case 44: return PN2_LDS_NP(4, 4);
+        case 42: return PN2_LDS_NP(4, 2);
+        default: return PN2_LDS_NP(2, 2);
     }
+#undef PN2_LDS_NP
 }
 
 // Large split (fp32-accurate) layers take 256 x 128 tiles (see dense_split_layer); the rows a
@@ -819,7 +881,7 @@ static int launch_dense_lds_tile(int tile, const DenseSplitArgs &A, int np, hipS
 // with it, 134.1-135.6k without (interleaved A/B x3).
 static bool dense_wide(const DenseSplitArgs &A, int np) {
     const int64_t wide_min = tuning().dense_wide_minwg;
-    return np == 3 && A.tiles % 4 == 0 && (A.M + 255) / 256 * (A.tiles / 4) >= wide_min;
+    return np >= 2 && A.tiles % 4 == 0 && (A.M + 255) / 256 * (A.tiles / 4) >= wide_min;
 }
 // the 4-wave tile's column tiles per wave: the widest that still leaves dense_minwg workgroups
 static int dense_ntc(const DenseSplitArgs &A) {
@@ -880,9 +942,12 @@ static int dense_split_layer(DenseSplitArgs &A, int np, hipStream_t st, bool pre
         }
     }
     int rc;
-    if (wide) rc = np == 1 ? launch_dense_split<4, 1, 8>(A, st) : launch_dense_split<4, 3, 8>(A, st);
+    if (wide) rc = np == 1 ? launch_dense_split<4, 1, 8>(A, st) : np == 2 ? launch_dense_split<4, 2, 8>(A, st)
+                                                                         : launch_dense_split<4, 3, 8>(A, st);
     else if (np == 1) rc = ntc == 4 ? launch_dense_split<4, 1>(A, st) : ntc == 2 ? launch_dense_split<2, 1>(A, st)
                                                                       : launch_dense_split<1, 1>(A, st);
+    else if (np == 2) rc = ntc == 4 ? launch_dense_split<4, 2>(A, st) : ntc == 2 ? launch_dense_split<2, 2>(A, st)
+                                                                      : launch_dense_split<1, 2>(A, st);
     else rc = ntc == 4 ? launch_dense_split<4, 3>(A, st) : ntc == 2 ? launch_dense_split<2, 3>(A, st)
                                                            : launch_dense_split<1, 3>(A, st);
     if (rc == PN2_OK && A.pool && A.pool_mode == 2 && A.norelu) {  // keys -> floats
@@ -916,6 +981,15 @@ int launch_layer0_prepass(const pn2_sa_src &s, const pn2_mlp_layer &L0, float *z
     return dense_split_layer(A, 3, st);
 }
 
+static thread_local int g_dense_planes = 3;
+int dense_last_planes() { return g_dense_planes; }
+
+// Workspace of the layer-by-layer path: two [M][w] fp32 halves, then two [ceil(M/32)][w/32]
+// uint max tables (the split-fp16 layers' activation scales, split_bf16.h)
+int64_t dense_split_ws_bytes(int64_t M, int64_t w) {
+    return 2 * M * w * 4 + 2 * ((M + 31) / 32) * ((w + 31) / 32) * 4;
+}
+
 // Widest hidden layer of a chain the split dense path runs layer by layer (0: not eligible).
 int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np) {
     if (np == 3 && tuning().mlp_f32) return 0;
@@ -936,7 +1010,16 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
                            int64_t K, int np, hipStream_t st) {
     const int64_t w = dense_split_width(s, layers, nlayers, np);
     if (w == 0) return 0;
-    if (nlayers > 1 && (!ws || ws_bytes < 2 * M * w * 4 || ((uintptr_t)ws & 15))) return 0;
+    if (nlayers > 1 && (!ws || ws_bytes < dense_split_ws_bytes(M, w) || ((uintptr_t)ws & 15))) return 0;
+    // The fp32-accurate hidden layers after the first (their rows are the workspace rows the
+    // layer before wrote, with its per-block maxima) run split fp16 (3 MFMAs per product);
+    // the first layer keeps split bf16 (its input comes from outside: no maxima).  A cloud's rows
+    // must start at a 32-row block (K % 32 == 0) so its scale never depends on other clouds.
+    // Tuning dense_f16 = 0: split bf16 everywhere.
+    const bool f16 = np == 3 && tuning().dense_f16 && K % 32 == 0;
+    const int64_t tw = (w + 31) / 32, nrb = (M + 31) / 32;
+    unsigned *maxtab = nlayers > 1 ? reinterpret_cast<unsigned *>(ws + 2 * M * w) : nullptr;
+    auto layer_np = [&](int l) { return (f16 && l >= 1) ? 2 : np; };
     auto make = [&](int l) {
         const bool last = l == nlayers - 1;
         DenseSplitArgs A;
@@ -967,6 +1050,13 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
         A.beta = layers[l].beta;
         A.tiles = (int)(layers[l].cout / 32);
         A.M = (int)M;
+        if (layer_np(l) == 2) {
+            A.w = split_f16_planes(layers[l].wt_split, layers[l].cout, A.kb);
+            A.wscale = split_f16_inv_scale(layers[l].wt_split, layers[l].cout, A.kb);
+            A.in_max = maxtab + ((l - 1) & 1) * nrb * tw;
+            A.in_tiles = (int)(layers[l - 1].cout / 32);
+        }
+        if (l < nlayers - 1 && layer_np(l + 1) == 2) A.out_max = maxtab + (l & 1) * nrb * tw;
         A.pool = last ? pool : 0;
         A.norelu = (layers[l].flags & PN2_LAYER_NO_RELU) ? 1 : 0;
         A.K = (int)K;
@@ -977,14 +1067,16 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
     // a last layer that pools by HBM atomics gets its output zeroed by the layer before it
     // (one launch fewer than a memset: PointNet-v1's max over N points, group_all over K > 256)
     DenseSplitArgs last = make(nlayers - 1);
-    const bool fold_zero = nlayers > 1 && last.pool && dense_needs_zero(last, np);
+    const bool fold_zero = nlayers > 1 && last.pool && dense_needs_zero(last, layer_np(nlayers - 1));
     if (s.zero_out && s.zero_count > 0) {  // the caller's side job rides on the last layer
         last.zero = s.zero_out;
         last.zrows = 1;
         last.zcols = s.zero_count;
         last.zstride = s.zero_count;
     }
+    int64_t flops[4] = {0, 0, 0, 0};
     for (int l = 0; l < nlayers; ++l) {
+        flops[layer_np(l)] += layers[l].cin * layers[l].cout;
         DenseSplitArgs A = l == nlayers - 1 ? last : make(l);
         if (fold_zero && l == nlayers - 2) {
             A.zero = last.out;
@@ -992,9 +1084,10 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
             A.zcols = 32 * (int64_t)last.tiles;
             A.zstride = last.ostride;
         }
-        const int rc = dense_split_layer(A, np, st, fold_zero && l == nlayers - 1);
+        const int rc = dense_split_layer(A, layer_np(l), st, fold_zero && l == nlayers - 1);
         if (rc != PN2_OK) return rc;
     }
+    g_dense_planes = flops[2] > flops[np] ? 2 : np;
     return 1;
 }
 

@@ -848,8 +848,8 @@ extern "C" int64_t pn2_sa_mlp_workspace_bytes(const pn2_sa_src *src, const pn2_m
     int64_t M = 0, K = 1;
     if (validate(src, layers, nlayers, M, K) != PN2_OK) return -1;
     const int64_t ds = nlayers > 1 ? dense_split_width(*src, layers, nlayers, 3) : 0;
-    return std::max(2 * M * std::max(ds, workspace_width(*src, layers, nlayers, M, K)) * 4,
-                    chain_prepass_bytes(*src, layers, nlayers, 3));
+    return std::max({dense_split_ws_bytes(M, ds), 2 * M * workspace_width(*src, layers, nlayers, M, K) * 4,
+                     chain_prepass_bytes(*src, layers, nlayers, 3)});
 }
 
 static int run_plan(const pn2_sa_src &cur, const pn2_mlp_layer *layers, int l0, int l1, int pool,
@@ -898,7 +898,7 @@ extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *la
     rc = try_launch_dense_split(*src, layers, nlayers, pool, out, ostride, workspace, workspace_bytes,
                                 M, K, 3, st);
     if (rc != 0) {
-        if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16, g_last_planes = 3;
+        if (rc > 0) g_last_path = PN2_PATH_SPLIT_BF16, g_last_planes = dense_last_planes();
         return rc < 0 ? rc : PN2_OK;
     }
     if ((rc = zero_side_job(*src, st)) != PN2_OK) return rc;
@@ -947,7 +947,7 @@ extern "C" int64_t pn2_sa_mlp_workspace_bytes_bf16(const pn2_sa_src *src,
     int64_t M = 0, K = 1;
     if (validate(src, layers, nlayers, M, K) != PN2_OK) return -1;
     const int64_t ds = nlayers > 1 ? dense_split_width(*src, layers, nlayers, 1) : 0;
-    return std::max(2 * M * ds * 4, chain_prepass_bytes(*src, layers, nlayers, 1));
+    return std::max(ds ? dense_split_ws_bytes(M, ds) : 0, chain_prepass_bytes(*src, layers, nlayers, 1));
 }
 
 extern "C" int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers,

@@ -191,6 +191,19 @@ __device__ __forceinline__ ActScale act_scale(float m) {
     return a;
 }
 
+// the NP = 2 planes (3-4) and the row scales inside a pn2_pack_layer_split_bf16 image of a layer
+// with `cout` outputs and `kbs` input k-blocks (include/pn2.h)
+__host__ __device__ inline const bf16x8 *split_f16_planes(const void *img, int64_t cout, int64_t kbs) {
+    return reinterpret_cast<const bf16x8 *>(static_cast<const char *>(img) + 3 * cout * kbs * 32);
+}
+__host__ __device__ inline const float *split_f16_inv_scale(const void *img, int64_t cout, int64_t kbs) {
+    return reinterpret_cast<const float *>(static_cast<const char *>(img) + 5 * cout * kbs * 32);
+}
+
+// NP = 2 dense layers (sa_dense.hip): the producing layer leaves, per 32-row block and 32-column
+// output tile, the largest |value| it wrote (uint bits, >= 0: order-preserving), so the consuming
+// layer's wave knows its 32 rows' scale before it splits its first k-block (pn2_internal.h's
+// wave_max_u32 reduces a lane's maxima; lane 0 stores the entry).
 typedef __attribute__((address_space(3))) void lds_void;
 
 }  // namespace pn2

@@ -367,3 +367,68 @@ def test_chain_split_f16_vs_oracle(case, f16):
     ratio = float((np.abs(got - want) / tol).max())
     print("case %d %s f16=%d: max err / tol %.4f" % (case, kind, f16, ratio))
     assert ratio < 0.1
+
+
+# split-fp16 dense layers (sa_dense.hip, NP = 2 for the layers after the first, the activation
+# scale from the producing layer's per-(32-row block, 32-column tile) maxima): group_all SA
+# layers.  (C, D, N = K, mlp, B, case)
+DENSE_F16 = [
+    (3, 256, 128, [256, 512, 1024], 4, "plain"),       # SSG sa3 (LDS tiles, LDS pool)
+    (10, 128, 512, [256, 512, 1024], 2, "plain"),      # translation_ssg sa2 (HBM atomics pool)
+    (3, 64, 64, [64, 128], 3, "plain"),                # register-staged tiles
+    (3, 64, 64, [64, 96, 128], 3, "hidden_1e4"),       # layer-1 inputs ~1e4
+    (3, 64, 64, [64, 96, 128], 3, "hidden_1e-5"),      # layer-1 inputs ~1e-5
+    (3, 64, 64, [64, 96, 128], 3, "tiny_row"),         # one layer-1 weight row 1e-6, var 1e-12
+    (3, 64, 64, [64, 96, 128], 3, "cloud_1e4"),        # cloud 1's hidden values 1e4 x cloud 0's
+    (3, 61, 64, [64, 128], 3, "K16"),                  # K = 16 points: split bf16 only
+]
+
+
+@pytest.mark.parametrize("f16", [1, 0])
+@pytest.mark.parametrize("case", range(len(DENSE_F16)))
+def test_dense_split_f16_vs_oracle(case, f16):
+    """The fp32-accurate dense layers after the first run split fp16 by default: within a tenth
+    of the 1e-5 tolerance of the float64 oracle, also at magnitudes outside fp16's range unless
+    scaled; a cloud's scale never depends on the other clouds of the batch (cloud_1e4: cloud 0
+    alone gives the same bits).  f16 = 0: tuning dense_f16 = 0 (split bf16)."""
+    import pn2
+    from pn2 import _lib, tuning
+    C, D, N, mlp, B, kind = DENSE_F16[case]
+    if kind == "K16":
+        N = 16
+    pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 1400 + case)
+    feat = torch.randn(B, N, D, generator=torch.Generator().manual_seed(1500 + case))
+    if kind == "cloud_1e4":
+        feat[1] *= 1e4
+    torch.manual_seed(1600 + case)
+    sa = pn2.PointNetSetAbstraction(None, None, None, C + D, mlp, True)
+    cases.randomize_bn(sa, 1700 + case)
+    with torch.no_grad():
+        if kind == "tiny_row":
+            sa.mlp_convs[1].weight[5] *= 1e-6
+            sa.mlp_convs[1].bias[5] *= 1e-6
+            sa.mlp_bns[1].running_mean[5] *= 1e-6
+            sa.mlp_bns[1].running_var[5] = 1e-12
+        if kind == "hidden_1e4":
+            sa.mlp_bns[0].bias.add_(1e4)
+        if kind == "hidden_1e-5":
+            sa.mlp_bns[0].weight.mul_(1e-5)
+            sa.mlp_bns[0].bias.mul_(1e-5)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous().to(DEV)
+    f = feat.permute(0, 2, 1).contiguous().to(DEV)
+    with torch.no_grad(), tuning.override(dense_f16=f16):
+        got = sa(x, f)[1].cpu().numpy()
+        torch.cuda.synchronize()
+        assert _lib.load().pn2_sa_mlp_last_path() == _lib.PATH_SPLIT_BF16
+        assert _lib.load().pn2_sa_mlp_last_planes() == (2 if f16 and kind != "K16" else 3)
+        if kind == "cloud_1e4":
+            alone = sa(x[:1], f[:1])[1].cpu().numpy()
+            np.testing.assert_array_equal(alone.view(np.uint32), got[:1].view(np.uint32))
+    rows = np.concatenate([pts.numpy(), feat.numpy()], -1)
+    want = oracle.mlp_max(rows[:, None], _oracle_layers(sa.mlp_convs, sa.mlp_bns))
+    got = got.transpose(0, 2, 1).astype(np.float64)
+    tol = 1e-5 * np.abs(want) + 1e-5 * np.abs(want).max(axis=(1, 2), keepdims=True)
+    ratio = float((np.abs(got - want) / tol).max())
+    print("case %d %s f16=%d: max err / tol %.4f" % (case, kind, f16, ratio))
+    assert ratio < 0.1
