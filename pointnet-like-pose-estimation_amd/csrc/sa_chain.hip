@@ -1328,7 +1328,11 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     // (r03, interleaved A/B x4, SSG K = 100): tuning compact_pool = 16 (the full pool, one
     // workgroup per CU fewer at sa1: 5 -> 4) and compact_stages = 3 (the 3-stage ring with the
     // 8-row pool wherever it keeps the workgroups per CU, i.e. sa2): 132.2-133.2k vs
-    // 119.5-129.7k clouds/s; MSG / POSE / STRESS within noise.
+    // 119.5-129.7k clouds/s; MSG / POSE / STRESS within noise.  r05, split fp16 (rings a third
+    // smaller): compact_stages = 2 -- the 3-stage sa2 instance spilled 16 B per lane (168-VGPR
+    // cap at 3 waves per SIMD; PMC write 7.9 vs 5.4 MB per call), eager sa1 49.0 -> 46.0 us, sa2
+    // 82.5 -> 81.6 us; pipelined SSG K = 20 166.3-167.2k -> 170.3-172.3k, K = 100 190.6-191.1k
+    // -> 190.3-194.7k, MSG / POSE / STRESS +1-2 % (tools/pmc_ab.sh, tools/args_ab.sh).
     int cks = 2, cprow = kUnitsPerWG;
     if (compact) {
         const int64_t cL = layers[2].cout;

@@ -54,7 +54,10 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--config", default="ssg")
+    ap.add_argument("--no-save", action="store_true", help="print only (A/B passes)")
     a = ap.parse_args()
+    if a.config not in FPS_PER_FORWARD:
+        raise SystemExit("pmc_traffic: no per-forward launch counts for config %r" % a.config)
     fetch = read(a.fetch_dir, "FETCH_SIZE")
     write = read(a.write_dir, "WRITE_SIZE")
     kernels = {}
@@ -78,12 +81,13 @@ def main():
     bq_total = sum(2 * 1024 * sum(v) for k, v in fetch.items() if "ball_query_kernel" in k) + \
         sum(1024 * sum(v) for k, v in write.items() if "ball_query_kernel" in k)
     bq_call = bq_total / (forwards * BQ_PER_FORWARD[a.config]) if forwards else None
-    out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    data = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    data[a.config] = {MLP_NAME.get(a.config, "pn2_sa_mlp_max_f32"): per_call,
-                      "pn2_ball_query_f32": bq_call, "forwards": forwards, "kernels": kernels,
-                      "note": "bytes per dispatch; FETCH_SIZE x2 (gfx950), KB->bytes"}
-    json.dump(data, open(out_path, "w"), indent=1, sort_keys=True)
+    if not a.no_save:
+        out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        data = json.load(open(out_path)) if os.path.exists(out_path) else {}
+        data[a.config] = {MLP_NAME.get(a.config, "pn2_sa_mlp_max_f32"): per_call,
+                          "pn2_ball_query_f32": bq_call, "forwards": forwards, "kernels": kernels,
+                          "note": "bytes per dispatch; FETCH_SIZE x2 (gfx950), KB->bytes"}
+        json.dump(data, open(out_path, "w"), indent=1, sort_keys=True)
     print(json.dumps({"config": a.config, "per_call_bytes": per_call, "forwards": forwards}))
     for k, v in kernels.items():
         print("%-60s %6d  fetch %12s  write %12s" % (k[:60], v["dispatches"],
