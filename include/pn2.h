@@ -19,6 +19,7 @@
  * Reference interfaces replaced (file:line in /root/reference):
  *   pn2_fps_f32            farthest_point_sample            model/pointnet2_utils.py:47-68
  *   pn2_fps_ws_f32         the same, any N (workspace)       model/pointnet2_utils.py:47-68
+ *   pn2_fps_host_ws_f32    the same, start drawn on the host model/pointnet2_utils.py:59
  *                          (+ index_points(points, fps_idx)  model/pointnet2_utils.py:106)
  *   pn2_ball_query_f32     query_ball_point + square_distance model/pointnet2_utils.py:70-90, 5-26
  *   pn2_pack_points_f32    torch.sum(points**2,-1) of square_distance model/pointnet2_utils.py:24-25
@@ -60,7 +61,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 15
+#define PN2_ABI_VERSION 16
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -132,6 +133,13 @@ int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb
                    int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
                    float *out_packed, float *pts_packed, void *workspace, int64_t workspace_bytes,
                    void *stream);
+/* The same with start_host[B] in HOST memory, as the reference draws it (pointnet2_utils.py:59:
+ * torch.randint on the CPU, then .to(device)): read during the call -- the caller may reuse it
+ * on return -- and checked (0 <= start < N, else PN2_EINVAL), no host->device copy. */
+int pn2_fps_host_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+                        int64_t sc, const int64_t *start_host, int64_t S, int64_t *out_idx,
+                        float *out_pts, float *out_packed, float *pts_packed, void *workspace,
+                        int64_t workspace_bytes, void *stream);
 
 /* Pack a [B,N,C] strided view into [B,N,cp] with its ssq (see above). */
 int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,

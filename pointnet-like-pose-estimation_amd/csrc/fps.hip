@@ -24,9 +24,22 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace pn2 {
 
 constexpr int kFpsMaxS = 8192;
+
+// The start indices of a launch: a device array (dev), or -- pn2_fps_host_ws_f32 -- up to
+// kFpsArgStarts values carried in the kernel arguments (the reference draws them on the host,
+// pointnet2_utils.py:59; as arguments they need no host->device copy, and the kernel after that
+// copy no longer waits for it: ~10 us per FPS call of the eager forward)
+constexpr int kFpsArgStarts = 256;
+struct FpsStart {
+    const int64_t *dev;
+    int v[kFpsArgStarts];
+};
+__device__ __forceinline__ int fps_start(const FpsStart &s, int b) { return s.dev ? (int)s.dev[b] : s.v[b]; }
 constexpr int kFpsLdsCloud = 128 * 1024;  // bytes of LDS a cloud copy may take
 
 // max over the first 16 lanes (row 0), result valid in every lane of row 0
@@ -63,7 +76,7 @@ extern "C" int pn2_debug_fps_wg(unsigned long long *out, unsigned *count) {
 template <int NT, int PPT, int CM, bool FIXED, bool LDSC, int CR = CM>
 __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, int N, int Crt,
                                                  int64_t sb, int64_t sn, int64_t sc, int kind,
-                                                 const int64_t *__restrict__ start, int S,
+                                                 const FpsStart start, int S,
                                                  int64_t *__restrict__ out_idx,
                                                  float *__restrict__ out_pts,
                                                  float *__restrict__ out_packed,
@@ -193,7 +206,7 @@ __global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, 
     }
 
     // ---- serial loop
-    int far = (int)start[b];
+    int far = fps_start(start, b);
     float c[CM];
 #pragma unroll
     for (int k = 0; k < CM; ++k) c[k] = (k < C) ? P[(int64_t)far * sn + (int64_t)k * sc] : 0.f;
@@ -372,7 +385,7 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 template <int CM, bool FIXED, bool DL>
 __global__ __launch_bounds__(kFpsStreamT) void fps_stream_kernel(
     const float *__restrict__ pts, int N, int Crt, int64_t sb, int64_t sn, int64_t sc, int kind,
-    const int64_t *__restrict__ start, int S, int64_t *__restrict__ out_idx, float *__restrict__ out_pts,
+    const FpsStart start, int S, int64_t *__restrict__ out_idx, float *__restrict__ out_pts,
     float *__restrict__ out_packed, float *__restrict__ pts_packed, int cp, unsigned *__restrict__ dist_ws) {
     constexpr int NT = kFpsStreamT, NW = NT / 64;
     __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
@@ -403,7 +416,7 @@ __global__ __launch_bounds__(kFpsStreamT) void fps_stream_kernel(
             for (int k = C + 1; k < cp; ++k) dst[k] = 0.f;
         }
     }
-    int far = (int)start[b];
+    int far = fps_start(start, b);
     float c[CM];
     point(far, c);
     __syncthreads();
@@ -500,7 +513,7 @@ extern "C" int64_t pn2_packed_stride(int64_t C) { return ((C + 1 + 3) / 4) * 4; 
 
 template <int NT, int PPT, int CM, bool FIXED, int CR = CM>
 static int launch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
-                      int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx,
+                      int64_t sc, const FpsStart &start, int64_t S, int64_t *out_idx,
                       float *out_pts, float *out_packed, float *pts_packed, hipStream_t st) {
     const int kind = layout_kind(sn, sc);
     constexpr int NW = NT / 64;
@@ -534,7 +547,7 @@ static int launch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t
 // (tuning experiments only).
 template <int CM, bool FIXED, int CAP>
 static int dispatch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
-                        int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx,
+                        int64_t sc, const FpsStart &start, int64_t S, int64_t *out_idx,
                         float *out_pts, float *out_packed, float *pts_packed, hipStream_t st) {
 #define A pts, B, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed, st
     const int64_t fnt = tuning().fps_threads, fppt = tuning().fps_ppt;
@@ -580,7 +593,7 @@ static bool fps_stream_dl(int64_t N) { return fps_stream_lds(N) <= (size_t)160 *
 
 template <int CM, bool FIXED>
 static int launch_fps_stream(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
-                             int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
+                             int64_t sc, const FpsStart &start, int64_t S, int64_t *out_idx, float *out_pts,
                              float *out_packed, float *pts_packed, unsigned *ws, hipStream_t st) {
     const int kind = layout_kind(sn, sc);
     const int cp = (int)pn2_packed_stride(C);
@@ -606,10 +619,8 @@ extern "C" int64_t pn2_fps_workspace_bytes(int64_t B, int64_t N, int64_t C, int6
     return (fps_resident(N, S) || fps_stream_dl(N)) ? 0 : B * N * 4;
 }
 
-extern "C" int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
-                              int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
-                              float *out_packed, float *pts_packed, void *workspace, int64_t workspace_bytes,
-                              void *stream) {
+static int fps_check(const float *pts, const int64_t *start, int64_t *out_idx, int64_t B, int64_t N,
+                     int64_t C, int64_t S, void *workspace, int64_t workspace_bytes) {
     PN2_REQUIRE(pts && start && out_idx, "pn2_fps_f32: null pointer");
     PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && S >= 1 && N < INT32_MAX && S < INT32_MAX,
                 "pn2_fps_f32: bad shape B=%lld N=%lld C=%lld S=%lld", (long long)B, (long long)N, (long long)C,
@@ -619,11 +630,15 @@ extern "C" int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C,
     PN2_REQUIRE(workspace_bytes >= need && (need == 0 || workspace),
                 "pn2_fps_f32: N=%lld needs pn2_fps_workspace_bytes = %lld bytes of workspace", (long long)N,
                 (long long)need);
-    if (B == 0) return PN2_OK;
-    hipStream_t st = as_stream(stream);
+    return PN2_OK;
+}
+
+static int fps_run(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn, int64_t sc,
+                   const FpsStart &start, int64_t S, int64_t *out_idx, float *out_pts, float *out_packed,
+                   float *pts_packed, void *workspace, hipStream_t st) {
 #define A pts, B, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed
     if (!fps_resident(N, S)) {
-        unsigned *ws = reinterpret_cast<unsigned *>(workspace);
+        unsigned *ws = static_cast<unsigned *>(workspace);
         if (C == 3) return launch_fps_stream<3, true>(A, ws, st);
         if (C == 10) return launch_fps_stream<10, true>(A, ws, st);
         return launch_fps_stream<kMaxC, false>(A, ws, st);
@@ -632,6 +647,45 @@ extern "C" int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C,
     if (C == 10) return dispatch_fps<10, true, 8192>(A, st);
     return dispatch_fps<kMaxC, false, 4096>(A, st);
 #undef A
+}
+
+extern "C" int pn2_fps_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+                              int64_t sc, const int64_t *start, int64_t S, int64_t *out_idx, float *out_pts,
+                              float *out_packed, float *pts_packed, void *workspace, int64_t workspace_bytes,
+                              void *stream) {
+    const int rc = fps_check(pts, start, out_idx, B, N, C, S, workspace, workspace_bytes);
+    if (rc != PN2_OK || B == 0) return rc;
+    FpsStart fs;
+    fs.dev = start;
+    return fps_run(pts, B, N, C, sb, sn, sc, fs, S, out_idx, out_pts, out_packed, pts_packed, workspace,
+                   as_stream(stream));
+}
+
+// start in host memory, read during the call (the caller may reuse it on return): carried in
+// the kernel arguments, kFpsArgStarts clouds per launch (a launch of that many clouds already
+// covers the chip's 256 CUs, so the split costs no concurrency)
+extern "C" int pn2_fps_host_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
+                                   int64_t sc, const int64_t *start_host, int64_t S, int64_t *out_idx,
+                                   float *out_pts, float *out_packed, float *pts_packed, void *workspace,
+                                   int64_t workspace_bytes, void *stream) {
+    int rc = fps_check(pts, start_host, out_idx, B, N, C, S, workspace, workspace_bytes);
+    if (rc != PN2_OK || B == 0) return rc;
+    for (int64_t b = 0; b < B; ++b)
+        PN2_REQUIRE(start_host[b] >= 0 && start_host[b] < N, "pn2_fps_f32: start[%lld] = %lld outside [0, %lld)",
+                    (long long)b, (long long)start_host[b], (long long)N);
+    const int cp = (int)pn2_packed_stride(C);
+    hipStream_t st = as_stream(stream);
+    FpsStart fs;
+    fs.dev = nullptr;
+    for (int64_t b0 = 0; b0 < B; b0 += kFpsArgStarts) {
+        const int64_t nb = std::min<int64_t>(kFpsArgStarts, B - b0);
+        for (int64_t j = 0; j < nb; ++j) fs.v[j] = (int)start_host[b0 + j];
+        rc = fps_run(pts + b0 * sb, nb, N, C, sb, sn, sc, fs, S, out_idx + b0 * S, out_pts ? out_pts + b0 * S * C : nullptr,
+                     out_packed ? out_packed + b0 * S * cp : nullptr, pts_packed ? pts_packed + b0 * N * cp : nullptr,
+                     workspace ? static_cast<unsigned *>(workspace) + b0 * N : nullptr, st);
+        if (rc != PN2_OK) return rc;
+    }
+    return PN2_OK;
 }
 
 extern "C" int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,

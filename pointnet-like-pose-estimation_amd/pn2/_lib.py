@@ -70,6 +70,8 @@ SIGNATURES = {
     "pn2_fps_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "pn2_fps_ws_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                               _i64, _vp]),
+    "pn2_fps_host_ws_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp,
+                                   _vp, _i64, _vp]),
     "pn2_pack_points_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pn2_ball_query_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp]),
     "pn2_ball_query_cnt_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp, _vp]),
@@ -121,7 +123,7 @@ SIGNATURES = {
                                _int, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 _lib = None
 
 

@@ -132,11 +132,17 @@ def cin_pad(cin: int) -> int:
 # ------------------------------------------------------------------------------ fps
 def fps_direct(points: Tensor, npoint: int, start: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """points [B,N,C] float32 (any strides), start [B] int64 -> (fps_idx [B,S] int64,
-    new_points [B,S,C], packed centroids [B,S,cp], packed points [B,N,cp])."""
+    new_points [B,S,C], packed centroids [B,S,cp], packed points [B,N,cp]).  A CPU start (the
+    reference's host draw) goes to pn2_fps_host_ws_f32 in the launch's arguments; a device start
+    (and any start under graph capture, whose replays must read a device slot) to pn2_fps_ws_f32."""
     _dev(points, "pn2::fps")
     B, N, C = points.shape
     cp = packed_stride(C)
-    start = start.to(device=points.device, dtype=torch.int64).contiguous()
+    host = start.device.type == "cpu" and not torch.cuda.is_current_stream_capturing()
+    if host:
+        start = start.to(dtype=torch.int64).contiguous()
+    else:
+        start = start.to(device=points.device, dtype=torch.int64).contiguous()
     idx = torch.empty(B, npoint, dtype=torch.int64, device=points.device)
     newp = torch.empty(B, npoint, C, dtype=torch.float32, device=points.device)
     cpk = torch.empty(B, npoint, cp, dtype=torch.float32, device=points.device)
@@ -146,7 +152,7 @@ def fps_direct(points: Tensor, npoint: int, start: Tensor) -> Tuple[Tensor, Tens
     # N = 40896 it keeps the running distances in this workspace
     nws = int(_L.pn2_fps_workspace_bytes(B, N, C, npoint))
     ws = torch.empty(max(nws, 0) // 4, dtype=torch.float32, device=points.device) if nws > 0 else None
-    _run("pn2_fps_f32", _L.pn2_fps_ws_f32,
+    _run("pn2_fps_f32", _L.pn2_fps_host_ws_f32 if host else _L.pn2_fps_ws_f32,
          (points.data_ptr(), B, N, C, sb, sn, sc, start.data_ptr(), npoint, idx.data_ptr(),
           newp.data_ptr(), cpk.data_ptr(), ppk.data_ptr(), 0 if ws is None else ws.data_ptr(),
           max(nws, 0), _stream(points)), points.device,

@@ -45,8 +45,10 @@ from . import train
 # ----------------------------------------------------------------------------- helpers
 def _draw_start(B, N, device):
     """The reference's FPS start draw: torch.randint(0, N, (B,), dtype=long) on the CPU default
-    generator (pointnet2_utils.py:59) -- one draw per FPS call, sliced when sharded."""
-    return shard.device_start(B, N, device)
+    generator (pointnet2_utils.py:59) -- one draw per FPS call, sliced when sharded.  A CPU
+    tensor (ops.fps_direct passes host starts in the launch's arguments), or a device slot under
+    graph capture."""
+    return shard.host_start(B, N, device)
 
 
 def _channels_last(feature):

@@ -103,6 +103,16 @@ def device_start(B, N, device):
     return draw_start(B, N).to(device, non_blocking=True)
 
 
+def host_start(B, N, device):
+    """The FPS start draw as the eager forward hands it to pn2_fps_host_ws_f32: a CPU int64
+    tensor (the launch carries the values in its kernel arguments -- no host->device copy), or,
+    inside a graph record/capture, what the installed start source returns (device_start)."""
+    rec = getattr(_state, "graph", None)
+    if rec is not None:
+        return rec(B, N, device)
+    return draw_start(B, N, pin=False)
+
+
 @contextlib.contextmanager
 def start_source(fn):
     """Route device_start(B, N, device) to fn for the duration (graph record/capture)."""

@@ -263,3 +263,29 @@ def test_fps_mid_shapes_exact(mid, C, N):
     with tuning.override(fps_mid=mid):
         idx, newp, cpk, ppk = torch.ops.pn2.fps(_to_dev_view(p), S, start.to(DEV))
     np.testing.assert_array_equal(idx.cpu().numpy(), want)
+
+
+# pn2_fps_host_ws_f32: the start draw in host memory, carried in the launch's arguments
+# (256 clouds per launch): the same bits as the device-start entry point, past the per-launch
+# cap (B = 300: two launches), on the streamed kernel, and checked on the host.
+@pytest.mark.parametrize("B,N,C,S", [(5, 1024, 3, 512), (300, 64, 3, 16), (3, 20000, 3, 8),
+                                     (4, 700, 10, 64), (2, 50000, 3, 4)])
+def test_fps_host_start_matches_device_start(B, N, C, S):
+    from pn2 import ops
+    pts = cases.as_layout(cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 31), "strided")
+    pd = _to_dev_view(pts)
+    start = torch.randint(0, N, (B,), generator=torch.Generator().manual_seed(B + N))
+    a = ops.fps_direct(pd, S, start)          # CPU tensor: host entry point
+    b = ops.fps_direct(pd, S, start.to(DEV))  # device entry point
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x.cpu().numpy().view(np.uint32 if x.dtype == torch.float32 else np.int64),
+                                      y.cpu().numpy().view(np.uint32 if y.dtype == torch.float32 else np.int64))
+    want = oracle.farthest_point_sample(pts[:1], S, start[:1])
+    np.testing.assert_array_equal(a[0][:1].cpu().numpy(), want)
+
+
+def test_fps_host_start_out_of_range_raises():
+    from pn2 import ops
+    pd = torch.rand(2, 64, 3, device=DEV)
+    with pytest.raises(RuntimeError, match="start"):
+        ops.fps_direct(pd, 8, torch.tensor([3, 64]))
