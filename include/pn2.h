@@ -245,6 +245,22 @@ int64_t pn2_layer_split_bytes(int64_t cout, int64_t cin, int64_t xyz);
 int pn2_pack_layer_split_bf16(const float *W, int64_t cout, int64_t cin, int64_t xyz,
                               int xyz_first, void *out, void *stream);
 
+/* Side job of an SA MLP call (pn2_sa_src.fps_side): the NEXT SA layer's farthest point sampling
+ * -- pn2_fps_host_ws_f32's arguments, start_host[B] in host memory (read during the call).  It
+ * runs inside the call's chain launch as extra workgroups when that launch allows it (its layer-0
+ * input register-resident; B <= 256 clouds of N <= 512 points with C = 3 or 10, S <= 8192, its
+ * LDS within the chain's), overlapping the MLP, else as its own launch on the same stream; the
+ * same results either way.  Its inputs must not be written by the call; it needs no workspace
+ * (pn2_fps_workspace_bytes == 0, else PN2_EINVAL).  In the reference the next layer samples
+ * after this one's MLP (pointnet2_cls_ssg.py:27-28; the same draw order, the draws taken on the
+ * host before the call). */
+typedef struct pn2_fps_side {
+    const float *pts; int64_t B, N, C, sb, sn, sc; /* points[b,n,c] = pts[b*sb + n*sn + c*sc]  */
+    const int64_t *start_host;                      /* [B], host memory                       */
+    int64_t S;
+    int64_t *out_idx; float *out_pts; float *out_packed; float *pts_packed; /* as pn2_fps_f32 */
+} pn2_fps_side;
+
 typedef struct pn2_sa_src {
     int mode; /* PN2_SRC_* */
     const float *pts; int64_t pb, pn, pc; /* points [B,N,C], any strides            */
@@ -262,6 +278,7 @@ typedef struct pn2_sa_src {
                                              done by one of the call's launches          */
     const int32_t *idx32;                 /* [B,S,K] int32 (pn2_ball_query_i32), read in
                                              place of idx when not NULL (group modes)    */
+    const pn2_fps_side *fps_side;         /* side job, or NULL (see pn2_fps_side)        */
 } pn2_sa_src;
 
 /* Bytes of workspace pn2_sa_mlp_max_f32 needs for this layer chain: 0 when the chain runs as

@@ -20,7 +20,7 @@
 //   v_readlane broadcasts its index/coordinates.  No second barrier, no global memory in the loop.
 // The sampled indices are kept in LDS and written, with the gathered centroids and the packed
 // (coords, ssq) records the ball query reads, after the serial loop.
-#include "pn2_internal.h"
+#include "fps_body.h"
 
 #include <stdlib.h>
 
@@ -28,337 +28,10 @@
 
 namespace pn2 {
 
-constexpr int kFpsMaxS = 8192;
-
-// The start indices of a launch: a device array (dev), or -- pn2_fps_host_ws_f32 -- up to
-// kFpsArgStarts values carried in the kernel arguments (the reference draws them on the host,
-// pointnet2_utils.py:59; as arguments they need no host->device copy, and the kernel after that
-// copy no longer waits for it: ~10 us per FPS call of the eager forward)
-constexpr int kFpsArgStarts = 256;
-struct FpsStart {
-    const int64_t *dev;
-    int v[kFpsArgStarts];
-};
-__device__ __forceinline__ int fps_start(const FpsStart &s, int b) { return s.dev ? (int)s.dev[b] : s.v[b]; }
-constexpr int kFpsLdsCloud = 128 * 1024;  // bytes of LDS a cloud copy may take
-
-// max over the first 16 lanes (row 0), result valid in every lane of row 0
-__device__ __forceinline__ unsigned row_max_u32(unsigned v) {
-    v = max(v, PN2_DPP(v, 0xB1));
-    v = max(v, PN2_DPP(v, 0x4E));
-    v = max(v, PN2_DPP(v, 0x141));
-    v = max(v, PN2_DPP(v, 0x140));
-    return v;
-}
-
-// LDSC: keep a copy of the cloud in LDS (N*CM floats) so the winner's coordinates are one
-// broadcast ds_read; otherwise they travel with the per-wave slots.
-#ifndef PN2_FPS_PRIO
-#define PN2_FPS_PRIO 3
-#endif
-//
-// CR: channels held in registers (CR = CM normally).  Large clouds whose points do not fit the
-// register file with every channel keep only xyz (CR = 3) or nothing (CR = 0) there and re-read
-// the other channels of their points from the input each iteration (slow, but any N up to
-// NT*PPT); a cloud whose extra channels are constant (the one-hot class) never reads them.
-#ifdef PN2_FPS_WGSTAMPS
-// Diagnostic builds only (tools/debug/fps_wg.py): s_memrealtime (100 MHz) at entry and exit of
-// every fps_kernel workgroup, in dispatch-counter order (65536 slots, wrapping)
-__device__ unsigned g_fps_wgctr;
-__device__ unsigned long long g_fps_wg[65536 * 2];
-extern "C" int pn2_debug_fps_wg(unsigned long long *out, unsigned *count) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(count, HIP_SYMBOL(g_fps_wgctr), sizeof(unsigned)) != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fps_wg), sizeof(g_fps_wg)) == hipSuccess ? 0 : -1;
-}
-#endif
-
 template <int NT, int PPT, int CM, bool FIXED, bool LDSC, int CR = CM>
-__global__ __launch_bounds__(NT) void fps_kernel(const float *__restrict__ pts, int N, int Crt,
-                                                 int64_t sb, int64_t sn, int64_t sc, int kind,
-                                                 const FpsStart start, int S,
-                                                 int64_t *__restrict__ out_idx,
-                                                 float *__restrict__ out_pts,
-                                                 float *__restrict__ out_packed,
-                                                 float *__restrict__ pts_packed, int cp) {
-    constexpr int NW = NT / 64;
-    static_assert(NW <= 16, "one 16-lane row reduces the wave slots");
-    // In the pipelined launch FPS shares every SIMD with the MLP kernels' waves, and its
-    // dependent chain (one short VALU burst, a reduction and a barrier per iteration) is the
-    // pipeline's critical path: its waves take issue priority over co-resident waves.
-    __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
-#ifdef PN2_FPS_WGSTAMPS
-    unsigned wg_slot = 0;
-    if (threadIdx.x == 0) {
-        wg_slot = atomicAdd(&g_fps_wgctr, 1u) & 65535u;
-        g_fps_wg[2 * wg_slot] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-    constexpr int SLOT = (CM + 2 + 3) & ~3;  // {max, index, coords...} padded to 16 bytes
-    const int C = FIXED ? CM : Crt;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int b = blockIdx.x;
-    const float *P = pts + (int64_t)b * sb;
-
+__global__ __launch_bounds__(NT) void fps_kernel(const FpsArgs F) {
     extern __shared__ __attribute__((aligned(16))) float fsm[];
-    int *sidx = reinterpret_cast<int *>(fsm);                          // [S]
-    unsigned long long *key = reinterpret_cast<unsigned long long *>(  // [3] (LDSC)
-        fsm + ((S + 3) & ~3));
-    float *slots = fsm + ((S + 3) & ~3) + 8;                            // [2][NW][SLOT] (!LDSC)
-    constexpr int CS = CM == 3 ? 4 : CM;  // cloud row stride (16-byte rows for xyz)
-    float *cloud = slots + (LDSC ? 0 : 2 * NW * SLOT);                  // [N][CS] (LDSC)
-
-    // ---- load the owned points into registers (and emit the packed copy for the ball query).
-    // Points are held in pairs (one packed v_pk_* op computes two distances).  Lanes past the
-    // end own padding points: coordinates 0, distance 0 -- they never beat a real point (real
-    // points precede them and ties go to the first index).
-    constexpr int PH = (PPT + 1) / 2;
-    static_assert(CR == CM || (CR <= 3 && !LDSC), "partial register residency: xyz or nothing");
-    constexpr int CQ = CR > 0 ? CR : 1;
-    // per channel, the owned points' coordinates as one register vector: pairs feed the packed
-    // distance ops, and a wave-uniform index selects one element with a single indexed move
-    // (s_set_gpr_idx) instead of a select chain
-    typedef float VQ __attribute__((ext_vector_type(2 * PH)));
-    VQ q[CQ];
-    unsigned dist[PPT];
-    // channel k of owned point j: registers, or the input (through `base`, which the serial
-    // loop launders every iteration so the compiler cannot hoist the re-reads out of it into
-    // registers the kernel does not have)
-    auto coord = [&](const float *base, int j, int k) -> float {
-        if (k < CR) return q[k < CQ ? k : 0][j];
-        const int n = tid * PPT + j;
-        return (j < PPT && n < N && k < C) ? base[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
-    };
-    // the packed copy first, point n on thread n % NT: each store instruction writes one
-    // contiguous run of records (a 16-byte record per lane for xyz), where the owned-points
-    // order below would scatter 4-byte stores 16*PPT bytes apart over a line per lane -- partial
-    // lines the L2 writes back, and re-reads, several times over.  The register loads after it
-    // hit the lines this pass brought into the L2.
-    if (pts_packed) {
-        for (int n = tid; n < N; n += NT) {
-            float pj[CM], sq[CM];
-#pragma unroll
-            for (int k = 0; k < CM; ++k) {
-                pj[k] = k < C ? P[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
-                sq[k] = __fmul_rn(pj[k], pj[k]);
-            }
-            const float s = layout_sum<CM>(sq, C, point_rule(kind, n, N));
-            float *dst = pts_packed + ((int64_t)b * N + n) * cp;
-            if (CM == 3 && cp == 4) {
-                *reinterpret_cast<float4 *>(dst) = make_float4(pj[0], pj[1], pj[2], s);
-            } else {
-#pragma unroll
-                for (int k = 0; k < CM; ++k)
-                    if (k < C) dst[k] = pj[k];
-                dst[C] = s;
-                for (int k = C + 1; k < cp; ++k) dst[k] = 0.f;
-            }
-        }
-    }
-    int rule[PH];  // a pair shares its rule: the strided tail starts at an even index
-#pragma unroll
-    for (int j = 0; j < 2 * PH; ++j) {
-        const int n = tid * PPT + j;
-        const bool valid = j < PPT && n < N;
-        float pj[CM];
-#pragma unroll
-        for (int k = 0; k < CM; ++k) {
-            pj[k] = (valid && k < C) ? P[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
-            if (k < CR) q[k < CQ ? k : 0][j] = pj[k];
-        }
-        if (j < PPT) dist[j] = valid ? __float_as_uint(1e10f) : 0u;
-        if ((j & 1) == 0) rule[j >> 1] = point_rule(kind, n, N);
-        if (LDSC && valid) {
-#pragma unroll
-            for (int k = 0; k < CS; ++k) cloud[n * CS + k] = k < CM ? pj[k] : 0.f;
-        }
-    }
-    if (LDSC && tid < 3) key[tid] = 0ull;
-
-    // ---- channels past xyz that are constant over the cloud (the pose heads' one-hot class:
-    // one label per cloud) contribute (v - v)^2 = +0 to every distance, and adding +0 leaves
-    // each of the reference's channel-sum orders equal to ((dx^2 + dy^2) + dz^2) -- so such a
-    // cloud runs the 3-channel loop, bit-identically.  Non-finite constants keep the full
-    // loop (inf - inf is NaN).
-    bool cst = true;
-    if constexpr (FIXED && CM > 3) {
-#pragma unroll
-        for (int k = 3; k < CM; ++k) {
-            const float v0 = P[(int64_t)k * sc];
-            cst = cst && __builtin_isfinite(v0);
-#pragma unroll
-            for (int j = 0; j < 2 * PH; ++j)
-                if (j < PPT && tid * PPT + j < N) cst = cst && (coord(P, j, k) == v0);
-        }
-    }
-    // block AND through a spare LDS word behind the key words (no static LDS: the cloud copy
-    // may use the whole 160 KB dynamically)
-    bool xyz_only = false;
-    if constexpr (FIXED && CM > 3) {
-        int *flag = reinterpret_cast<int *>(fsm + ((S + 3) & ~3) + 6);
-        if (tid == 0) *flag = 1;
-        __syncthreads();
-        if (!cst) *flag = 0;  // every writer stores 0: a benign race
-        __syncthreads();
-        xyz_only = *flag != 0;
-    }
-
-    // ---- serial loop
-    int far = fps_start(start, b);
-    float c[CM];
-#pragma unroll
-    for (int k = 0; k < CM; ++k) c[k] = (k < C) ? P[(int64_t)far * sn + (int64_t)k * sc] : 0.f;
-    __syncthreads();
-
-    for (int i = 0;; ++i) {
-        if (tid == 0) sidx[i] = far;
-        if (i == S - 1) break;
-        const float *Pl = P;
-        if constexpr (CR < CM) asm volatile("" : "+s"(Pl));
-
-        // distances (two points per packed op) and the running min -- branchless
-#pragma unroll
-        for (int h = 0; h < PH; ++h) {
-            pn2_f2 dd;
-            if (xyz_only) {
-                pn2_f2 s3[3];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const pn2_f2 qk = k < CR ? pn2_f2{q[k < CQ ? k : 0][2 * h], q[k < CQ ? k : 0][2 * h + 1]}
-                                             : pn2_f2{coord(Pl, 2 * h, k), coord(Pl, 2 * h + 1, k)};
-                    const pn2_f2 d = qk - c[k];
-                    s3[k] = d * d;
-                }
-                dd = (s3[0] + s3[1]) + s3[2];
-            } else {
-                pn2_f2 sq[CM];
-#pragma unroll
-                for (int k = 0; k < CM; ++k) {
-                    const pn2_f2 qk = k < CR ? pn2_f2{q[k < CQ ? k : 0][2 * h], q[k < CQ ? k : 0][2 * h + 1]}
-                                             : pn2_f2{coord(Pl, 2 * h, k), coord(Pl, 2 * h + 1, k)};
-                    const pn2_f2 d = qk - c[k];
-                    sq[k] = d * d;
-                }
-                if constexpr (FIXED && CM == 3) dd = seq_sum<CM>(sq, C);  // every rule agrees for C=3
-                else dd = layout_sum<CM>(sq, C, rule[h]);
-            }
-            // strict '<' update == min on the (non-negative) float bits; padding stays 0
-            dist[2 * h] = min(dist[2 * h], __float_as_uint(dd.x));
-            if (2 * h + 1 < PPT) dist[2 * h + 1] = min(dist[2 * h + 1], __float_as_uint(dd.y));
-        }
-        unsigned bv = dist[0];
-#pragma unroll
-        for (int j = 1; j < PPT; ++j) bv = max(bv, dist[j]);
-        // wave: max value, then its first lane (contiguous ownership -> smallest index)
-        const unsigned wv = wave_max_u32(bv);
-        const int ol = (int)__builtin_ctzll(__ballot(bv == wv));
-        // the owner lane's first point holding the max, wave-uniform: one compare per point
-        // writes its lane mask straight to an SGPR pair, the scan over the owner's bit is SALU
-        int bj = PPT - 1;
-#pragma unroll
-        for (int j = PPT - 2; j >= 0; --j)
-            if ((__ballot(dist[j] == wv) >> ol) & 1ull) bj = j;
-        if constexpr (LDSC) {
-            if constexpr (NW == 1) {
-                far = ol * PPT + bj;
-            } else {
-                // one 64-bit LDS max per wave: key = dist bits : ~index (max dist, then first
-                // index).  key[i%3] is reset one iteration ahead; its last reader passed the
-                // previous barrier.
-                if (lane == ol) {
-                    const unsigned idx = (unsigned)(tid * PPT + bj);
-                    atomicMax(&key[i % 3], ((unsigned long long)wv << 32) | (0xFFFFFFFFu - idx));
-                }
-                if (tid == 64) key[(i + 1) % 3] = 0ull;
-                __syncthreads();
-                far = __builtin_amdgcn_readfirstlane((int)(0xFFFFFFFFu - (unsigned)key[i % 3]));
-            }
-#pragma unroll
-            for (int k = 0; k < CM; ++k) c[k] = cloud[far * CS + k];
-        } else {
-            float bc[CM];
-#pragma unroll
-            for (int k = 0; k < CM; ++k) {
-                if (k < CR) {
-                    bc[k] = q[k < CQ ? k : 0][bj];  // meaningful in the owner lane
-                } else if (k < 3 || !xyz_only) {  // the owner lane reads its point's other channels
-                    const int n = tid * PPT + bj;
-                    bc[k] = (lane == ol && n < N && k < C) ? Pl[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
-                } else {
-                    bc[k] = 0.f;  // a constant channel: its difference is +0 whatever c[k] is
-                }
-            }
-            if constexpr (NW == 1) {
-                far = ol * PPT + bj;
-#pragma unroll
-                for (int k = 0; k < CM; ++k)
-                    c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bc[k]), ol));
-                continue;
-            }
-            const int par = i & 1;
-            if (lane == ol) {
-                float *sl = slots + (par * NW + wave) * SLOT;
-                sl[0] = __uint_as_float(wv);
-                sl[1] = __int_as_float(tid * PPT + bj);
-#pragma unroll
-                for (int k = 0; k < CM; ++k) sl[2 + k] = bc[k];
-            }
-            __syncthreads();
-            unsigned rv = 0u;
-            int ri = 0x7FFFFFFF;
-            float rc[CM];
-#pragma unroll
-            for (int k = 0; k < CM; ++k) rc[k] = 0.f;
-            if (lane < NW) {
-                const float *sl = slots + (par * NW + lane) * SLOT;
-                rv = __float_as_uint(sl[0]);
-                ri = __float_as_int(sl[1]);
-#pragma unroll
-                for (int k = 0; k < CM; ++k) rc[k] = sl[2 + k];
-            }
-            const unsigned gv = __builtin_amdgcn_readlane(row_max_u32(rv), 0);
-            const int gw = (int)__builtin_ctzll(__ballot(lane < NW && rv == gv));
-            far = __builtin_amdgcn_readlane(ri, gw);
-#pragma unroll
-            for (int k = 0; k < CM; ++k)
-                c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rc[k]), gw));
-        }
-    }
-    __syncthreads();
-
-    // ---- outputs: indices, gathered centroids (index_points), packed centroids
-    for (int i = tid; i < S; i += NT) {
-        const int n = sidx[i];
-        out_idx[(int64_t)b * S + i] = n;
-        if (out_pts || out_packed) {
-            float q[CM], sq[CM];
-#pragma unroll
-            for (int k = 0; k < CM; ++k) {
-                q[k] = (k < C) ? P[(int64_t)n * sn + (int64_t)k * sc] : 0.f;
-                sq[k] = __fmul_rn(q[k], q[k]);
-            }
-            if (out_pts) {
-                float *o = out_pts + ((int64_t)b * S + i) * C;
-#pragma unroll
-                for (int k = 0; k < CM; ++k)
-                    if (k < C) o[k] = q[k];
-            }
-            if (out_packed) {
-                // index_points returns a contiguous tensor: contiguous-layout ssq
-                float *o = out_packed + ((int64_t)b * S + i) * cp;
-#pragma unroll
-                for (int k = 0; k < CM; ++k)
-                    if (k < C) o[k] = q[k];
-                o[C] = contig_sum<CM>(sq, C);
-                for (int k = C + 1; k < cp; ++k) o[k] = 0.f;
-            }
-        }
-    }
-#ifdef PN2_FPS_WGSTAMPS
-    if (threadIdx.x == 0) g_fps_wg[2 * wg_slot + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
+    fps_block<NT, PPT, CM, FIXED, LDSC, CR>(F, (int)blockIdx.x, fsm);
 }
 
 // ------------------------------------------------------------------------- streamed FPS
@@ -511,33 +184,47 @@ using namespace pn2;
 
 extern "C" int64_t pn2_packed_stride(int64_t C) { return ((C + 1 + 3) / 4) * 4; }
 
+// the FpsArgs of a launch (or side job) over points pts[b*sb + n*sn + c*sc]
+FpsArgs pn2::fps_args(const float *pts, int64_t N, int64_t C, int64_t sb, int64_t sn, int64_t sc,
+                 const FpsStart &start, int64_t S, int64_t *out_idx, float *out_pts, float *out_packed,
+                 float *pts_packed) {
+    FpsArgs F;
+    F.pts = pts;
+    F.N = (int)N;
+    F.C = (int)C;
+    F.sb = sb;
+    F.sn = sn;
+    F.sc = sc;
+    F.kind = layout_kind(sn, sc);
+    F.S = (int)S;
+    F.out_idx = out_idx;
+    F.out_pts = out_pts;
+    F.out_packed = out_packed;
+    F.pts_packed = pts_packed;
+    F.cp = (int)pn2_packed_stride(C);
+    F.start = start;
+    return F;
+}
+
 template <int NT, int PPT, int CM, bool FIXED, int CR = CM>
 static int launch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
                       int64_t sc, const FpsStart &start, int64_t S, int64_t *out_idx,
                       float *out_pts, float *out_packed, float *pts_packed, hipStream_t st) {
-    const int kind = layout_kind(sn, sc);
-    constexpr int NW = NT / 64;
-    constexpr int SLOT = (CM + 2 + 3) & ~3;
-    const size_t head = (size_t)((S + 3) & ~3) * 4 + 32;
-    const size_t cloud = (size_t)N * (CM == 3 ? 4 : CM) * 4;
+    const FpsArgs F = fps_args(pts, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed);
+    const size_t head = fps_block_lds(NT, CM, true, 0, S);
+    const size_t cloud = fps_block_lds(NT, CM, true, N, S) - head;
     const bool ldsc = CR == CM && cloud <= (size_t)kFpsLdsCloud && head + cloud <= (size_t)160 * 1024;
-    const size_t lds = head + (ldsc ? cloud : (size_t)2 * NW * SLOT * 4);
+    const size_t lds = fps_block_lds(NT, CM, ldsc, N, S);
     if constexpr (CR != CM) {
-        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, false, CR>), dim3((unsigned)B), dim3(NT), lds, st,
-                           pts, (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx, out_pts,
-                           out_packed, pts_packed, (int)pn2_packed_stride(C));
+        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, false, CR>), dim3((unsigned)B), dim3(NT), lds, st, F);
     } else if (ldsc) {
         static const hipError_t attr = hipFuncSetAttribute(
             reinterpret_cast<const void *>(&fps_kernel<NT, PPT, CM, FIXED, true>),
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)attr;
-        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, true>), dim3((unsigned)B), dim3(NT), lds, st, pts,
-                           (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx, out_pts,
-                           out_packed, pts_packed, (int)pn2_packed_stride(C));
+        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, true>), dim3((unsigned)B), dim3(NT), lds, st, F);
     } else {
-        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, false>), dim3((unsigned)B), dim3(NT), lds, st, pts,
-                           (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx, out_pts,
-                           out_packed, pts_packed, (int)pn2_packed_stride(C));
+        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, false>), dim3((unsigned)B), dim3(NT), lds, st, F);
     }
     PN2_LAUNCH_CHECK("fps_kernel");
     return PN2_OK;
@@ -694,6 +381,41 @@ extern "C" int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, in
                            void *stream) {
     return pn2_fps_ws_f32(pts, B, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed, nullptr, 0,
                           stream);
+}
+
+// ------------------------------------------------------------------------- FPS side jobs
+bool &pn2::fps_side_taken() {
+    static thread_local bool taken = false;
+    return taken;
+}
+
+int pn2::fps_side_check(const pn2_fps_side &f) {
+    PN2_REQUIRE(f.start_host, "pn2_fps_side: null start_host");
+    const int rc = fps_check(f.pts, f.start_host, f.out_idx, f.B, f.N, f.C, f.S, nullptr, 0);
+    if (rc != PN2_OK) return rc;
+    for (int64_t b = 0; b < f.B; ++b)
+        PN2_REQUIRE(f.start_host[b] >= 0 && f.start_host[b] < f.N,
+                    "pn2_fps_side: start[%lld] = %lld outside [0, %lld)", (long long)b,
+                    (long long)f.start_host[b], (long long)f.N);
+    return PN2_OK;
+}
+
+int pn2::fps_side_launch(const pn2_fps_side &f, hipStream_t st) {
+    return pn2_fps_host_ws_f32(f.pts, f.B, f.N, f.C, f.sb, f.sn, f.sc, f.start_host, f.S, f.out_idx, f.out_pts,
+                               f.out_packed, f.pts_packed, nullptr, 0, st);
+}
+
+// The side job as workgroups of a chain launch (sa_chain_kernel<., ., 1, ., .>: fps_block<256, 2,
+// C, true, true>, one workgroup per cloud): false when its shape does not fit that instance or
+// its LDS exceeds the chain's
+bool pn2::fps_side_block_args(const pn2_fps_side &f, size_t lds_avail, FpsArgs &F) {
+    if (f.B < 1 || f.B > kFpsArgStarts || f.N > 512 || f.S > kFpsMaxS || (f.C != 3 && f.C != 10)) return false;
+    if (fps_block_lds(256, (int)f.C, true, f.N, f.S) > lds_avail) return false;
+    FpsStart fs;
+    fs.dev = nullptr;
+    for (int64_t b = 0; b < f.B; ++b) fs.v[b] = (int)f.start_host[b];
+    F = fps_args(f.pts, f.N, f.C, f.sb, f.sn, f.sc, fs, f.S, f.out_idx, f.out_pts, f.out_packed, f.pts_packed);
+    return true;
 }
 
 extern "C" int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,

@@ -41,6 +41,7 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(chain_prepass, 1)    /* 0: no layer-0 pre-pass (wide first layers of a chain)        */ \
     X(compact, 1)          /* 0: no compact neighbourhoods (every padded row computed)     */ \
     X(compact_pool, 16)     /* LDS pool rows of compact chain launches (0: automatic)       */ \
+    X(fps_side, 1)         /* 0: FPS side jobs as their own launches, not in the chain's    */ \
     X(compact_stages, 2)   /* weight-ring stages of compact chain launches (2 or 3)        */ \
     X(bq_waves, 16)        /* ball query waves per workgroup (8 or 16; 0: 16 for xyz clouds  */ \
                            /* of >= 2048 points, else 8 -- the pipelines' choice)           */ \
@@ -92,6 +93,12 @@ int chain_last_planes();
 // sa_dense.hip: split-bf16 layer-by-layer path for group_all / dense-row chains
 int64_t dense_split_width(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int np);
 int64_t dense_split_ws_bytes(int64_t M, int64_t w);
+// FPS side jobs of SA MLP calls (pn2_fps_side, csrc/fps.hip): argument check, the separate
+// launch (when no chain launch took the job), and the calling thread's "taken" flag that
+// try_launch_chain sets when its launch runs the job
+int fps_side_check(const pn2_fps_side &f);
+int fps_side_launch(const pn2_fps_side &f, hipStream_t st);
+bool &fps_side_taken();
 // planes per operand carrying most of the flops of the calling thread's last dense-layer call
 int dense_last_planes();
 int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlayers, int pool,
@@ -109,10 +116,22 @@ int64_t chain_prepass_bytes(const pn2_sa_src &s, const pn2_mlp_layer *layers, in
 //  strided (stride_n == 1):  n < 16*floor(N/16) -> sequential; tail -> row_sum order.
 // `a` is a register array; C is runtime (<= CM).
 // Element-wise adds in round-to-nearest.  The vector overload (two points per packed
-// v_pk_add_f32) relies on -ffp-contract=off in the translation units that use it.
+// v_pk_add_f32) is a plain add under `fp contract(off)` (no product may be fused into it).
 typedef float pn2_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
-__device__ __forceinline__ pn2_f2 add_rn(pn2_f2 a, pn2_f2 b) { return a + b; }
+// (__fadd_rn / __fmul_rn are plain operators in the HIP headers: contractible in a unit built
+// with contraction on, e.g. the SA chain unit that runs the FPS side job)
+__device__ __forceinline__ float add_rn(float a, float b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+__device__ __forceinline__ float mul_rn(float a, float b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
+__device__ __forceinline__ pn2_f2 add_rn(pn2_f2 a, pn2_f2 b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
 
 template <int CM, typename T>
 __device__ __forceinline__ T seq_sum(const T (&a)[CM], int C) {

@@ -31,6 +31,7 @@
 // wave on the chip) are copied by global_load_lds into a small per-wave LDS ring a few steps
 // ahead of use (see ring_issue below); BN scale/shift are staged in LDS once per workgroup.
 #include "pn2_internal.h"
+#include "fps_body.h"
 #include "split_bf16.h"
 
 #include <algorithm>
@@ -82,6 +83,11 @@ struct ChainArgs {
     // weight ring's stage count (2 or 3)
     int pool_rows;
     int ks;
+    // side job (pn2_fps_side): workgroups 0 .. fps_blocks-1 of the launch run the next SA
+    // layer's FPS, one cloud each (fps_nb clouds; fps_blocks rounded up to a multiple of 8 so the
+    // chain's own workgroups keep their XCD placement), the rest the chain (KB0M == 1 instances)
+    FpsArgs fps;
+    int fps_blocks, fps_nb;
 };
 
 // Timeline stamps (diagnostic builds only: -DPN2_CHAIN_STAMPS, tools/debug/chain_stamps.py):
@@ -299,7 +305,18 @@ __global__ __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_e
     // a cloud's workgroups on one XCD: its rows gather the same points (and the pre-pass wrote
     // that cloud's z rows from the same XCD, see sa_dense.hip)
     PN2_STAMP(0);
-    const int bid = (int)xcd_contiguous(blockIdx.x, gridDim.x);
+    if constexpr (KB0M == 1) {
+        // the FPS side job: dispatched first (lowest ids), at issue priority 3 (fps_block) beside
+        // the chain's waves on its CUs; no barrier of the chain is reached by these workgroups
+        if ((int)blockIdx.x < A.fps_blocks) {
+            if ((int)blockIdx.x < A.fps_nb) {
+                if (A.fps.C == 3) fps_block<256, 2, 3, true, true>(A.fps, (int)blockIdx.x, reinterpret_cast<float *>(csm));
+                else fps_block<256, 2, 10, true, true>(A.fps, (int)blockIdx.x, reinterpret_cast<float *>(csm));
+            }
+            return;
+        }
+    }
+    const int bid = (int)xcd_contiguous(blockIdx.x - (unsigned)A.fps_blocks, gridDim.x - (unsigned)A.fps_blocks);
     const int slab = bid * kChainWaves + wave;
     const pn2_sa_src &s = A.src;
     const ChainLayer &L0 = A.L[0], &L1 = A.L[1], &L2 = A.L[2];
@@ -1436,15 +1453,26 @@ int try_launch_chain(const pn2_sa_src &s, const pn2_mlp_layer *layers, int nlaye
     const size_t bn_bytes = (size_t)2 * 4 * (layers[0].cout + layers[1].cout + coutL);
     A.lds_ring = (int)((A.lds_bn + bn_bytes + 15) / 16 * 16);
     lds = (size_t)A.lds_ring + (size_t)(compact ? cks : kStages) * stage_b;
+    // the caller's FPS side job rides on this launch when the instance has it (KB0M == 1: the
+    // xyz-only first layers, i.e. sa1) and it fits the chain's LDS
+    unsigned lgrid = grid;
+    if (s.fps_side && KB0M == 1 && tuning().fps_side && fps_side_block_args(*s.fps_side, lds, A.fps)) {
+        A.fps_nb = (int)s.fps_side->B;
+        A.fps_blocks = (A.fps_nb + 7) / 8 * 8;
+        lgrid += (unsigned)A.fps_blocks;
+    }
     int rc = PN2_EUNSUPPORTED;
 #define PN2_CHAIN_GO(a, b, c)                                                             \
     if (T0 == a && T1 == b && KB0M == c)                                                  \
-        rc = npk == 3 ? launch_chain_sig<a, b, c, 3>(A, grid, lds, st)                    \
-           : npk == 2 ? launch_chain_sig<a, b, c, 2>(A, grid, lds, st)                    \
-                      : launch_chain_sig<a, b, c, 1>(A, grid, lds, st);
+        rc = npk == 3 ? launch_chain_sig<a, b, c, 3>(A, lgrid, lds, st)                   \
+           : npk == 2 ? launch_chain_sig<a, b, c, 2>(A, lgrid, lds, st)                   \
+                      : launch_chain_sig<a, b, c, 1>(A, lgrid, lds, st);
     PN2_CHAIN_SIGS(PN2_CHAIN_GO)
 #undef PN2_CHAIN_GO
-    if (rc == PN2_OK) g_last_planes = npk;
+    if (rc == PN2_OK) {
+        g_last_planes = npk;
+        if (A.fps_blocks) fps_side_taken() = true;
+    }
     return rc == PN2_OK ? 1 : rc;
 }
 

@@ -878,9 +878,9 @@ static int zero_side_job(const pn2_sa_src &s, hipStream_t st) {
     return e == hipSuccess ? PN2_OK : set_error(PN2_EHIP, "pn2_sa_mlp_max: zero_out: %s", hipGetErrorString(e));
 }
 
-extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers,
-                                  int nlayers, int pool, float *out, int64_t ostride,
-                                  float *workspace, int64_t workspace_bytes, void *stream) {
+static int mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers,
+                       int nlayers, int pool, float *out, int64_t ostride,
+                       float *workspace, int64_t workspace_bytes, void *stream) {
     int64_t M = 0, K = 1;
     int rc = validate(src, layers, nlayers, M, K);
     if (rc != PN2_OK) return rc;
@@ -950,9 +950,9 @@ extern "C" int64_t pn2_sa_mlp_workspace_bytes_bf16(const pn2_sa_src *src,
     return std::max(ds ? dense_split_ws_bytes(M, ds) : 0, chain_prepass_bytes(*src, layers, nlayers, 1));
 }
 
-extern "C" int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers,
-                                   int nlayers, int pool, float *out, int64_t ostride,
-                                   float *workspace, int64_t workspace_bytes, void *stream) {
+static int mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers,
+                        int nlayers, int pool, float *out, int64_t ostride,
+                        float *workspace, int64_t workspace_bytes, void *stream) {
     int64_t M = 0, K = 1;
     int rc = validate(src, layers, nlayers, M, K);
     if (rc != PN2_OK) return rc;
@@ -978,4 +978,37 @@ extern "C" int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *l
     g_last_path = PN2_PATH_BF16;
     g_last_planes = 1;
     return PN2_OK;
+}
+
+// The entry points: the MLP, and the caller's FPS side job (pn2_fps_side) -- inside the chain
+// launch when try_launch_chain took it, else as its own launch after the MLP's
+template <typename F>
+static int with_fps_side(const pn2_sa_src *src, void *stream, F &&mlp) {
+    const pn2_fps_side *side = src ? src->fps_side : nullptr;
+    if (side) {
+        const int rc = fps_side_check(*side);
+        if (rc != PN2_OK) return rc;
+    }
+    fps_side_taken() = false;
+    const int rc = mlp();
+    const bool taken = fps_side_taken();
+    fps_side_taken() = false;
+    if (rc != PN2_OK || !side || taken) return rc;
+    return fps_side_launch(*side, as_stream(stream));
+}
+
+extern "C" int pn2_sa_mlp_max_f32(const pn2_sa_src *src, const pn2_mlp_layer *layers,
+                                  int nlayers, int pool, float *out, int64_t ostride,
+                                  float *workspace, int64_t workspace_bytes, void *stream) {
+    return with_fps_side(src, stream, [&] {
+        return mlp_max_f32(src, layers, nlayers, pool, out, ostride, workspace, workspace_bytes, stream);
+    });
+}
+
+extern "C" int pn2_sa_mlp_max_bf16(const pn2_sa_src *src, const pn2_mlp_layer *layers,
+                                   int nlayers, int pool, float *out, int64_t ostride,
+                                   float *workspace, int64_t workspace_bytes, void *stream) {
+    return with_fps_side(src, stream, [&] {
+        return mlp_max_bf16(src, layers, nlayers, pool, out, ostride, workspace, workspace_bytes, stream);
+    });
 }

@@ -33,6 +33,12 @@ class MlpLayer(ctypes.Structure):
                 ("wt_split", _vp), ("flags", _i64)]
 
 
+class FpsSide(ctypes.Structure):
+    _fields_ = [("pts", _vp), ("B", _i64), ("N", _i64), ("C", _i64), ("sb", _i64), ("sn", _i64), ("sc", _i64),
+                ("start_host", _vp), ("S", _i64),
+                ("out_idx", _vp), ("out_pts", _vp), ("out_packed", _vp), ("pts_packed", _vp)]
+
+
 class SaSrc(ctypes.Structure):
     _fields_ = [
         ("mode", _int),
@@ -45,6 +51,7 @@ class SaSrc(ctypes.Structure):
         ("cnt", _vp),
         ("zero_out", _vp), ("zero_count", _i64),
         ("idx32", _vp),
+        ("fps_side", _vp),
     ]
 
 

@@ -124,10 +124,60 @@ def provide(entries):
         _tls.entries = prev
 
 
+def provided(module):
+    """Whether pn2.pipeline provided `module`'s geometry for the current forward."""
+    entries = getattr(_tls, "entries", None)
+    return bool(entries) and id(module) in entries
+
+
+# ----------------------------------------------------------------------------- FPS lookahead
+# In an eager forward the next SA layer's FPS reads only this layer's centroids: the heads wrap
+# sa1 -> sa2 in fps_ahead(sa1, sa2), and sa1's MLP call then runs sa2's FPS as a side job of the
+# same launch (pn2_fps_side: extra workgroups of the chain kernel, overlapping the MLP; ~40 us
+# off SSG's serial chain).  sa2's start is drawn right after sa1's own, where the reference draws
+# it relative to every other draw (nothing draws in between).  Not inside graph capture, with
+# geometry provided by pn2.pipeline, or with the geometry stream on.
+@contextlib.contextmanager
+def fps_ahead(first, nxt):
+    prev = getattr(_tls, "pair", None)
+    _tls.pair = (first, nxt)
+    try:
+        yield
+    finally:
+        _tls.pair = prev
+        ahead = getattr(_tls, "ahead", None)
+        if ahead:
+            ahead.pop(id(nxt), None)  # not taken (an exception on the way): dropped
+
+
+def ahead_of(module):
+    """The module whose FPS `module`'s MLP call may run (fps_ahead), or None."""
+    pair = getattr(_tls, "pair", None)
+    if pair is None or pair[0] is not module or enabled() or provided(pair[1]):
+        return None
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    return pair[1]
+
+
+def put_ahead(module, pts, newp, cpk, ppk):
+    """Register `module`'s FPS results, computed ahead on `pts` (its forward's points)."""
+    if not hasattr(_tls, "ahead"):
+        _tls.ahead = {}
+    _tls.ahead[id(module)] = (pts.data_ptr(), newp, cpk, ppk, None)
+
+
 def take(module, pts):
-    """The provided FPS results for `module` called on `pts`, or None when nothing is provided.
-    A provided entry whose recorded input differs from `pts` is an error (the precomputed
-    sampling -- and the RNG draws behind it -- would not match this call)."""
+    """The provided (pn2.pipeline) or computed-ahead (fps_ahead) FPS results for `module` called
+    on `pts`, or None.  An entry whose recorded input differs from `pts` is an error (the
+    precomputed sampling -- and the RNG draws behind it -- would not match this call)."""
+    ahead = getattr(_tls, "ahead", None)
+    if ahead and id(module) in ahead:
+        ptr, newp, cpk, ppk, idxs = ahead.pop(id(module))
+        if ptr != pts.data_ptr():
+            raise RuntimeError("pn2.geometry.fps_ahead: the SA module was called on a different "
+                               "point tensor than the centroids its FPS was computed on")
+        return newp, cpk, ppk, idxs
     entries = getattr(_tls, "entries", None)
     if not entries or id(module) not in entries:
         return None

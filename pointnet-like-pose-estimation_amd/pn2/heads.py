@@ -25,6 +25,7 @@ import torch.nn.functional as F
 from .pointnet2_utils import PointNetSetAbstraction as SA
 from .pointnet2_utils import PointNetSetAbstractionMsg as SAMsg
 from .pointnet2_utils import _needs_autograd
+from . import geometry
 from . import ops
 from . import tuning
 from .pointnet_utils import _fold_linear, linear_bn
@@ -100,8 +101,9 @@ class ClsSSG(_FCHead):
 
     def forward(self, points):
         B = points.shape[0]
-        l1p, l1f = self.sa1(points, None)
-        l2p, l2f = self.sa2(l1p, l1f)
+        with geometry.fps_ahead(self.sa1, self.sa2):  # sa2's FPS inside sa1's MLP launch
+            l1p, l1f = self.sa1(points, None)
+            l2p, l2f = self.sa2(l1p, l1f)
         _, l3f = self.sa3(l2p, l2f)
         x, pred = self._fc_log_softmax(l3f.reshape(B, 1024))
         return x, l3f, pred
@@ -117,8 +119,9 @@ class ClsMSG(_FCHead):
 
     def forward(self, points):
         B = points.shape[0]
-        l1p, l1f = self.sa1(points, None)
-        l2p, l2f = self.sa2(l1p, l1f)
+        with geometry.fps_ahead(self.sa1, self.sa2):  # sa2's FPS inside sa1's MLP launch
+            l1p, l1f = self.sa1(points, None)
+            l2p, l2f = self.sa2(l1p, l1f)
         _, l3f = self.sa3(l2p, l2f)
         x, pred = self._fc_log_softmax(l3f.reshape(B, 1024))
         return x, l3f, pred
@@ -135,8 +138,9 @@ class RotationSSG(_FCHead):
 
     def forward(self, points):
         B = points.shape[0]
-        l1p, l1f = self.sa1(points, None)
-        l2p, l2f = self.sa2(l1p, l1f)
+        with geometry.fps_ahead(self.sa1, self.sa2):  # sa2's FPS inside sa1's MLP launch
+            l1p, l1f = self.sa1(points, None)
+            l2p, l2f = self.sa2(l1p, l1f)
         _, l3f = self.sa3(l2p, l2f)
         return self._fc(l3f.reshape(B, 1024))
 
@@ -174,8 +178,9 @@ class RotationMSG(_FCHead):
 
     def forward(self, points):
         B = points.shape[0]
-        l1p, l1f = self.sa1(points, None)
-        l2p, l2f = self.sa2(l1p, l1f)
+        with geometry.fps_ahead(self.sa1, self.sa2):  # sa2's FPS inside sa1's MLP launch
+            l1p, l1f = self.sa1(points, None)
+            l2p, l2f = self.sa2(l1p, l1f)
         _, l3f = self.sa3(l2p, l2f)
         return self._fc(l3f.reshape(B, 1024))
 

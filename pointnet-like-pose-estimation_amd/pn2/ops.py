@@ -18,6 +18,7 @@ Ops (reference code each replaces, in /root/reference/model/pointnet2_utils.py):
   pn2::sa_mlp_max_    gathered shared MLP + max :167-172, :211-218 (writes into `out`)
 """
 import contextlib
+import ctypes
 import threading
 from typing import List, Optional, Tuple
 
@@ -399,12 +400,43 @@ def _src(mode, points, feature, centers, idx, rows, B, N, C, D, S, K, cnt=None):
     return s
 
 
+def fps_side_job(points: Tensor, npoint: int, start: Tensor):
+    """The next SA layer's farthest point sampling as a side job of an SA MLP call (pn2_fps_side):
+    points [B,N,C] (any strides), start [B] int64 on the CPU -> (job, (fps_idx, new_points,
+    packed centroids, packed points)); pass `job` as sa_mlp_max_impl(..., fps_side=job).  The
+    outputs are fps_direct's, filled by the MLP call's launches."""
+    _dev(points, "pn2::fps")
+    B, N, C = points.shape
+    cp = packed_stride(C)
+    start = start.to(dtype=torch.int64).contiguous()
+    if start.device.type != "cpu" or start.shape != (B,):
+        raise ValueError("pn2::fps side job: start must be a [B] CPU tensor")
+    dev = points.device
+    outs = (torch.empty(B, npoint, dtype=torch.int64, device=dev),
+            torch.empty(B, npoint, C, dtype=torch.float32, device=dev),
+            torch.empty(B, npoint, cp, dtype=torch.float32, device=dev),
+            torch.empty(B, N, cp, dtype=torch.float32, device=dev))
+    sb, sn, sc = points.stride()
+    job = _lib.FpsSide(points.data_ptr(), B, N, C, sb, sn, sc, start.data_ptr(), npoint,
+                       *(t.data_ptr() for t in outs))
+    job._keep = (points, start)  # alive until the MLP call has read them
+    return job, outs
+
+
 def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature: Optional[Tensor],
                 centers: Optional[Tensor], idx: Optional[Tensor], wts: List[Tensor],
                 alphas: List[Tensor], betas: List[Tensor], cins: List[int],
                 splits: List[Tensor], precision: str = "fp32", flags: Optional[List[int]] = None,
                 rows: Optional[Tensor] = None, pool: bool = True,
                 cnt: Optional[Tensor] = None, zero: Optional[Tensor] = None) -> None:
+    """sa_mlp_max_impl without a side job (the signature torch.library registers)."""
+    sa_mlp_max_impl(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits,
+                    precision, flags, rows, pool, cnt, zero)
+
+
+def sa_mlp_max_impl(out, mode, points, feature, centers, idx, wts, alphas, betas, cins, splits,
+                    precision="fp32", flags=None, rows=None, pool=True, cnt=None, zero=None,
+                    fps_side=None):
     """Fused gather -> MLP (conv1x1+BN+ReLU)* -> max over each group, written channels-last
     into `out` ([G, >=cout] view with unit column stride; G = B*S groups, or B for
     group_all).  mode: 0 SSG grouping, 1 MSG grouping, 2 group_all, 3 rows (`rows` [B, R, cin]
@@ -415,7 +447,8 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
     last-layer output ([M, >=cout], group_all / rows sources).  cnt: the ball query's
     distinct-neighbour counts ([B, S] int32, grouping modes) -- only those rows of each group are
     computed (the rest repeat the first neighbour; same result).  zero: a contiguous float32
-    tensor one of the call's launches fills with zeros (group_all's new_points)."""
+    tensor one of the call's launches fills with zeros (group_all's new_points).  fps_side: a
+    fps_side_job() the call also runs (sa_mlp_max_impl only; the SA modules' lookahead)."""
     if precision not in PRECISIONS:
         raise ValueError("pn2::sa_mlp_max_: precision must be one of %s" % (PRECISIONS,))
     bf16 = precision == "bf16"
@@ -448,6 +481,8 @@ def sa_mlp_max_direct(out: Tensor, mode: int, points: Optional[Tensor], feature:
         if zero.dtype != torch.float32 or not zero.is_contiguous() or zero.device != dev_t.device:
             raise ValueError("pn2::sa_mlp_max_: zero must be a contiguous float32 device tensor")
         src.zero_out, src.zero_count = zero.data_ptr(), zero.numel()
+    if fps_side is not None:
+        src.fps_side = ctypes.addressof(fps_side)
     n = len(wts)
     layers = (MlpLayer * n)()
     for i in range(n):

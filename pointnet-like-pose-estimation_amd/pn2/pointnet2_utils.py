@@ -51,6 +51,22 @@ def _draw_start(B, N, device):
     return shard.host_start(B, N, device)
 
 
+def _fps_ahead(module, new_points):
+    """The side job that runs the next SA layer's FPS (geometry.fps_ahead) on this layer's
+    centroids `new_points` [B, S, C] inside this layer's MLP call, or None: registered so the next
+    layer's forward takes its results instead of sampling."""
+    nxt = geometry.ahead_of(module)
+    if nxt is None or getattr(nxt, "group_all", False) or nxt.point_number is None:
+        return None
+    if _needs_autograd(nxt, new_points) or shard.recording():  # (graph records: device starts)
+        return None
+    B, N, _ = new_points.shape
+    start = shard.host_start(B, N, new_points.device)
+    job, (_, newp, cpk, ppk) = ops.fps_side_job(new_points, nxt.point_number, start)
+    geometry.put_ahead(nxt, new_points, newp, cpk, ppk)
+    return job
+
+
 def _channels_last(feature):
     """[B, D, N] feature -> a [B, N, D] view with unit channel stride (copy only if needed)."""
     f = feature.permute(0, 2, 1)
@@ -263,8 +279,8 @@ class PointNetSetAbstraction(nn.Module):
                 idx, cnt = ops.ball_query_direct(ppk, cpk, C, self.radius, K, True)
             span.finish([new_points], [new_points, idx, cnt])
         out = torch.empty(B * S, cout, device=dev, dtype=torch.float32)
-        ops.sa_mlp_max_direct(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
-                        cins, splits, _precision(self), cnt=cnt)
+        ops.sa_mlp_max_impl(out, _lib.SRC_GROUP_XYZ_FIRST, pts, feat, new_points, idx, wts, als, bes,
+                            cins, splits, _precision(self), cnt=cnt, fps_side=_fps_ahead(self, new_points))
         return new_points.permute(0, 2, 1), out.view(B, S, cout).permute(0, 2, 1)
 
     def _forward_autograd(self, points, feature):
@@ -333,11 +349,14 @@ class PointNetSetAbstractionMsg(nn.Module):
         out = torch.empty(B * S, total, device=dev, dtype=torch.float32)
         prec = _precision(self)
         col = 0
+        side = _fps_ahead(self, new_points)  # rides on the longest scale's launch (largest K)
+        longest = max(range(len(idxs)), key=lambda i: self.sample_number_list[i])
         for i, (idx, cnt) in enumerate(idxs):
             wts, als, bes, cins, splits = chains[i]
             cout = wts[-1].shape[1]
-            ops.sa_mlp_max_direct(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
-                            new_points, idx, wts, als, bes, cins, splits, prec, cnt=cnt)
+            ops.sa_mlp_max_impl(out[:, col:col + cout], _lib.SRC_GROUP_FEAT_FIRST, pts, feat,
+                                new_points, idx, wts, als, bes, cins, splits, prec, cnt=cnt,
+                                fps_side=side if i == longest else None)
             col += cout
         return new_points.permute(0, 2, 1), out.view(B, S, total).permute(0, 2, 1)
 

@@ -103,6 +103,11 @@ def device_start(B, N, device):
     return draw_start(B, N).to(device, non_blocking=True)
 
 
+def recording():
+    """Whether a graph record/capture's start source is installed (start_source)."""
+    return getattr(_state, "graph", None) is not None
+
+
 def host_start(B, N, device):
     """The FPS start draw as the eager forward hands it to pn2_fps_host_ws_f32: a CPU int64
     tensor (the launch carries the values in its kernel arguments -- no host->device copy), or,
