@@ -383,6 +383,13 @@ extern "C" int pn2_fps_f32(const float *pts, int64_t B, int64_t N, int64_t C, in
                           stream);
 }
 
+#ifdef PN2_FPS_STAMPS
+extern "C" int pn2_debug_fps_stamps(unsigned long long *out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fps_stamps), sizeof(g_fps_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // ------------------------------------------------------------------------- FPS side jobs
 bool &pn2::fps_side_taken() {
     static thread_local bool taken = false;

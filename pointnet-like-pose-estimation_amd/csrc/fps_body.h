@@ -30,6 +30,8 @@ __device__ __forceinline__ int fps_start(const FpsStart &s, int b) {
     return v;
 }
 constexpr int kFpsLdsCloud = 128 * 1024;  // bytes of LDS a cloud copy may take
+// bytes of the cross-wave key words ([3] u64, triple-buffered) + the block flag, 16-aligned
+constexpr int kFpsKeyRegion = (3 * 8 + 4 + 15) / 16 * 16;
 
 
 // One launch's (or side job's) FPS arguments: points[b, n, c] = pts[b*sb + n*sn + c*sc]
@@ -50,10 +52,28 @@ FpsArgs fps_args(const float *pts, int64_t N, int64_t C, int64_t sb, int64_t sn,
                  float *pts_packed);
 bool fps_side_block_args(const pn2_fps_side &f, size_t lds_avail, FpsArgs &F);
 
+// Per-link cycle breakdown of the serial loop (diagnostic builds only, -DPN2_FPS_STAMPS:
+// tools/debug/fps_stamps.py).  Every wave of workgroups 0-3 accumulates s_memtime deltas per
+// link, each stamp first waiting for its LDS operations (so a link's cost includes the latency
+// of its own LDS traffic): 0 loop top, 1 distances + running min, 2 lane max + wave max, 3
+// owner lane + point (ballots), 4 key atomic + reset, 5 barrier, 6 key read, 7 centroid read.
+#ifdef PN2_FPS_STAMPS
+static __device__ unsigned long long g_fps_stamps[4 * 16 * 8];
+#define PN2_FPS_T(i)                                                 \
+    do {                                                             \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");           \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
+        st_acc[i] += t_ - st_last;                                   \
+        st_last = t_;                                                \
+    } while (0)
+#else
+#define PN2_FPS_T(i) do {} while (0)
+#endif
+
 // LDS bytes of fps_block<NT, PPT, CM, FIXED, LDSC> for N points and S samples
 __host__ __device__ inline size_t fps_block_lds(int NT, int CM, bool ldsc, int64_t N, int64_t S) {
     const int NW = NT / 64, SLOT = (CM + 2 + 3) & ~3;
-    const size_t head = (size_t)((S + 3) & ~3) * 4 + 32;
+    const size_t head = (size_t)((S + 3) & ~3) * 4 + kFpsKeyRegion;
     const size_t cloud = (size_t)N * (CM == 3 ? 4 : CM) * 4;
     return head + (ldsc ? cloud : (size_t)2 * NW * SLOT * 4);
 }
@@ -107,7 +127,7 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
     int *sidx = reinterpret_cast<int *>(fsm);                          // [S]
     unsigned long long *key = reinterpret_cast<unsigned long long *>(  // [3] (LDSC)
         fsm + ((S + 3) & ~3));
-    float *slots = fsm + ((S + 3) & ~3) + 8;                            // [2][NW][SLOT] (!LDSC)
+    float *slots = fsm + ((S + 3) & ~3) + kFpsKeyRegion / 4;            // [2][NW][SLOT] (!LDSC)
     constexpr int CS = CM == 3 ? 4 : CM;  // cloud row stride (16-byte rows for xyz)
     float *cloud = slots + (LDSC ? 0 : 2 * NW * SLOT);                  // [N][CS] (LDSC)
 
@@ -198,7 +218,7 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
     // may use the whole 160 KB dynamically)
     bool xyz_only = false;
     if constexpr (FIXED && CM > 3) {
-        int *flag = reinterpret_cast<int *>(fsm + ((S + 3) & ~3) + 6);
+        int *flag = reinterpret_cast<int *>(key + 3);
         if (tid == 0) *flag = 1;
         __syncthreads();
         if (!cst) *flag = 0;  // every writer stores 0: a benign race
@@ -213,7 +233,11 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
     for (int k = 0; k < CM; ++k) c[k] = (k < C) ? P[(int64_t)far * sn + (int64_t)k * sc] : 0.f;
     __syncthreads();
 
+#ifdef PN2_FPS_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last = __builtin_amdgcn_s_memtime();
+#endif
     for (int i = 0;; ++i) {
+        PN2_FPS_T(0);
         if (tid == 0) sidx[i] = far;
         if (i == S - 1) break;
         const float *Pl = P;
@@ -249,11 +273,13 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
             dist[2 * h] = min(dist[2 * h], __float_as_uint(dd.x));
             if (2 * h + 1 < PPT) dist[2 * h + 1] = min(dist[2 * h + 1], __float_as_uint(dd.y));
         }
+        PN2_FPS_T(1);
         unsigned bv = dist[0];
 #pragma unroll
         for (int j = 1; j < PPT; ++j) bv = max(bv, dist[j]);
         // wave: max value, then its first lane (contiguous ownership -> smallest index)
         const unsigned wv = wave_max_u32(bv);
+        PN2_FPS_T(2);
         const int ol = (int)__builtin_ctzll(__ballot(bv == wv));
         // the owner lane's first point holding the max, wave-uniform: one compare per point
         // writes its lane mask straight to an SGPR pair, the scan over the owner's bit is SALU
@@ -268,16 +294,21 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
                 // one 64-bit LDS max per wave: key = dist bits : ~index (max dist, then first
                 // index).  key[i%3] is reset one iteration ahead; its last reader passed the
                 // previous barrier.
+                PN2_FPS_T(3);
                 if (lane == ol) {
                     const unsigned idx = (unsigned)(tid * PPT + bj);
                     atomicMax(&key[i % 3], ((unsigned long long)wv << 32) | (0xFFFFFFFFu - idx));
                 }
                 if (tid == 64) key[(i + 1) % 3] = 0ull;
+                PN2_FPS_T(4);
                 __syncthreads();
+                PN2_FPS_T(5);
                 far = __builtin_amdgcn_readfirstlane((int)(0xFFFFFFFFu - (unsigned)key[i % 3]));
+                PN2_FPS_T(6);
             }
 #pragma unroll
             for (int k = 0; k < CM; ++k) c[k] = cloud[far * CS + k];
+            PN2_FPS_T(7);
         } else {
             float bc[CM];
 #pragma unroll
@@ -328,6 +359,10 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
         }
     }
     __syncthreads();
+#ifdef PN2_FPS_STAMPS
+    if (b < 4 && lane == 0)
+        for (int k = 0; k < 8; ++k) g_fps_stamps[(b * 16 + wave) * 8 + k] = st_acc[k];
+#endif
 
     // ---- outputs: indices, gathered centroids (index_points), packed centroids
     for (int i = tid; i < S; i += NT) {
