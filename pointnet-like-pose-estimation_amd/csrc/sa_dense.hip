@@ -98,15 +98,39 @@ struct DenseSplitArgs {
     unsigned *out_max;
 };
 
-// NP = 2: this wave's activation scale (rows rb*32 .. rb*32+31 of a rows-mode input)
+// NP = 2: this wave's activation scale, from the max |value| of its 32 rows (rb*32 ..): the
+// producing layer's per-(row block, tile) maxima (in_max, rows mode), or -- a first layer over
+// points (mode 1: group_all, the pre-pass) -- the rows themselves, read once more before the
+// main loop ([xyz | features], L2-resident; lane (r, h) takes every other channel of row r)
+__device__ __forceinline__ unsigned abs_bits(float x) { return __float_as_uint(x) & 0x7FFFFFFFu; }
 template <int NP>
 __device__ __forceinline__ ActScale dense_act_scale(const DenseSplitArgs &A, int rb, int lane) {
     if constexpr (NP != 2) {
         return ActScale{1.f, 1.f};
     } else {
         unsigned m = 0;
-        if (32 * rb < A.M)
-            for (int t = lane; t < A.in_tiles; t += 64) m = max(m, A.in_max[(int64_t)rb * A.in_tiles + t]);
+        if (A.in_max) {
+            if (32 * rb < A.M)
+                for (int t = lane; t < A.in_tiles; t += 64) m = max(m, A.in_max[(int64_t)rb * A.in_tiles + t]);
+        } else {
+            const int h = lane >> 5, R = 32 * rb + (lane & 31);
+            if (R < A.M) {
+                const int b = R / A.N, n = R - b * A.N;
+                const float *p = A.pts + (int64_t)b * A.pb + (int64_t)n * A.pn;
+                for (int c = h; c < A.C; c += 2) m = max(m, abs_bits(p[(int64_t)c * A.pc]));
+                if (A.feat) {
+                    const float *f = A.feat + (int64_t)b * A.fb + (int64_t)n * A.fn;
+                    if (A.vec) {
+                        for (int c = 4 * h; c < A.D; c += 8) {
+                            const cfloatx4 q = *reinterpret_cast<const cfloatx4 *>(f + c);
+                            m = max(max(m, max(abs_bits(q[0]), abs_bits(q[1]))), max(abs_bits(q[2]), abs_bits(q[3])));
+                        }
+                    } else {
+                        for (int c = h; c < A.D; c += 2) m = max(m, abs_bits(f[c]));
+                    }
+                }
+            }
+        }
         return act_scale(__uint_as_float(wave_max_u32(m)));
     }
 }
@@ -126,9 +150,8 @@ __device__ __forceinline__ Split split_scaled(const float (&x)[8], float up) {
 // wave's activation down-scale)
 template <int NP>
 __device__ __forceinline__ float dense_alpha(const DenseSplitArgs &A, int col, float down) {
-    if (A.raw) return 1.f;
-    if constexpr (NP == 2) return A.alpha[col] * A.wscale[col] * down;
-    else return A.alpha[col];
+    if constexpr (NP == 2) return (A.raw ? 1.f : A.alpha[col]) * A.wscale[col] * down;
+    else return A.raw ? 1.f : A.alpha[col];
 }
 
 // Signed max through unsigned atomics: key() is monotone from float order to uint order (and
@@ -371,7 +394,7 @@ void dense_split_kernel(const DenseSplitArgs A) {
                 const int row = slab_row + (q & 3) + 8 * (q >> 2) + 4 * h;
                 if (row < A.M) {
                     const float y = __builtin_fmaf(acc[i][q], al, be);
-                    const float v = A.raw ? acc[i][q] : (A.norelu ? y : chain_relu(y));
+                    const float v = A.raw ? acc[i][q] * al : (A.norelu ? y : chain_relu(y));
                     A.out[(int64_t)row * A.ostride + col] = v;
                     tmax = max(tmax, __float_as_uint(v) & 0x7FFFFFFFu);
                 }
@@ -616,13 +639,13 @@ void dense_lds_kernel(const DenseSplitArgs A) {
             const int ch = (j & 3) + 8 * (j >> 2) + 4 * h;
             x[j] = ch < A.C ? prow[(int64_t)ch * A.pc] : 0.f;
         }
-        const Split xs = splitN<NP>(x);
+        const Split xs = split_scaled<NP>(x, asc.up);
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             const bf16x8 *wq = A.w + (int64_t)(ct0 + i) * A.kb * 64 + lane;
             Split w;
             w.h = wq[0];
-            w.m = NP == 3 ? wq[plane] : w.h;
+            w.m = NP >= 2 ? wq[plane] : w.h;
             w.l = NP == 3 ? wq[2 * plane] : w.h;
             acc[i] = mma_wb<NP>(xs, w, acc[i]);
         }
@@ -749,7 +772,7 @@ void dense_lds_kernel(const DenseSplitArgs A) {
                 const int row = slab_row + (q & 3) + 8 * (q >> 2) + 4 * h;
                 if (row < A.M) {
                     const float y = __builtin_fmaf(acc[i][q], al, be);
-                    const float v = A.raw ? acc[i][q] : (A.norelu ? y : chain_relu(y));
+                    const float v = A.raw ? acc[i][q] * al : (A.norelu ? y : chain_relu(y));
                     A.out[(int64_t)row * A.ostride + col] = v;
                     tmax = max(tmax, __float_as_uint(v) & 0x7FFFFFFFu);
                 }
@@ -978,6 +1001,13 @@ int launch_layer0_prepass(const pn2_sa_src &s, const pn2_mlp_layer &L0, float *z
     A.out = z;
     A.ostride = L0.cout;
     A.raw = 1;
+    // split fp16 with the scale from each 32-point block's own [xyz | features] (a cloud's points
+    // fill whole blocks); tuning dense_f16 = 0: split bf16
+    if (tuning().dense_f16 >= 2 && s.N % 32 == 0) {
+        A.w = split_f16_planes(L0.wt_split, L0.cout, A.kb);
+        A.wscale = split_f16_inv_scale(L0.wt_split, L0.cout, A.kb);
+        return dense_split_layer(A, 2, st);
+    }
     return dense_split_layer(A, 3, st);
 }
 
@@ -1019,7 +1049,10 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
     const bool f16 = np == 3 && tuning().dense_f16 && K % 32 == 0;
     const int64_t tw = (w + 31) / 32, nrb = (M + 31) / 32;
     unsigned *maxtab = nlayers > 1 ? reinterpret_cast<unsigned *>(ws + 2 * M * w) : nullptr;
-    auto layer_np = [&](int l) { return (f16 && l >= 1) ? 2 : np; };
+    // the first layer over points (group_all) takes its scale from its own rows when a cloud's
+    // points fill whole 32-row blocks
+    const bool f16_first = f16 && tuning().dense_f16 >= 2 && s.mode == PN2_SRC_GROUP_ALL && s.N % 32 == 0;
+    auto layer_np = [&](int l) { return (f16 && l >= 1) || (f16_first && l == 0) ? 2 : np; };
     auto make = [&](int l) {
         const bool last = l == nlayers - 1;
         DenseSplitArgs A;
@@ -1053,8 +1086,10 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
         if (layer_np(l) == 2) {
             A.w = split_f16_planes(layers[l].wt_split, layers[l].cout, A.kb);
             A.wscale = split_f16_inv_scale(layers[l].wt_split, layers[l].cout, A.kb);
-            A.in_max = maxtab + ((l - 1) & 1) * nrb * tw;
-            A.in_tiles = (int)(layers[l - 1].cout / 32);
+            if (l > 0) {
+                A.in_max = maxtab + ((l - 1) & 1) * nrb * tw;
+                A.in_tiles = (int)(layers[l - 1].cout / 32);
+            }
         }
         if (l < nlayers - 1 && layer_np(l + 1) == 2) A.out_max = maxtab + (l & 1) * nrb * tw;
         A.pool = last ? pool : 0;

@@ -305,17 +305,20 @@ F16 = [
     (3, 0, 16, 64, 512, 0.3, [32, 32, 64], True, "plain"),          # MSG row order (xyz only)
     (3, 96, 32, 32, 256, 0.35, [64, 64, 128], True, "plain"),       # MSG, wide layer 0 -> pre-pass
     (3, 16, 16, 64, 512, 0.3, [32, 32, 64], True, "streamed"),      # streamed layer 0: split bf16
+    (3, 128, 64, 64, 512, 0.4, [128, 128, 256], False, "feat_1e4"),  # pre-pass rows ~1e4 (split fp16)
+    (3, 128, 64, 64, 512, 0.4, [128, 128, 256], False, "feat_1e-5"),  # pre-pass rows ~1e-5
 ]
 
 
-@pytest.mark.parametrize("f16", [1, 0])
+@pytest.mark.parametrize("f16", [2, 1, 0])
 @pytest.mark.parametrize("case", range(len(F16)))
 def test_chain_split_f16_vs_oracle(case, f16):
     """The fp32-accurate chains run split fp16 (3 MFMAs per product) by default: within 1e-5 of
     the float64 oracle with margin (the worst error stays below a tenth of the tolerance, as the
     6-MFMA split bf16 does), including inputs whose magnitudes leave fp16's range unless both
     operands are scaled: coordinates x1e3 / x1e-4, a weight row of 1e-6 whose BN scale is 1e6,
-    hidden activations ~1e4 / ~1e-5.  f16 = 0: tuning chain_f16 = 0 (split bf16)."""
+    hidden activations ~1e4 / ~1e-5.  f16 = 0: tuning chain_f16 = 0 (split bf16); f16 = 2: the
+    layer-0 pre-pass in split fp16 as well."""
     import pn2
     from pn2 import _lib, tuning
     C, D, K, S, N, radius, mlp, msg, kind = F16[case]
@@ -325,6 +328,8 @@ def test_chain_split_f16_vs_oracle(case, f16):
     radius = radius * scale
     gen = torch.Generator().manual_seed(600 + case)
     feat = torch.randn(B, N, D, generator=gen) if D else None
+    if kind in ("feat_1e4", "feat_1e-5"):
+        feat *= {"feat_1e4": 1e4, "feat_1e-5": 1e-5}[kind]
     torch.manual_seed(700 + case)
     if msg:
         sa = pn2.PointNetSetAbstractionMsg(S, [K], [radius], D, [mlp])
@@ -347,7 +352,8 @@ def test_chain_split_f16_vs_oracle(case, f16):
     sa = sa.to(DEV).eval()
     x = pts.permute(0, 2, 1).contiguous()
     f = feat.permute(0, 2, 1).contiguous() if D else None
-    with tuning.override(chain_f16=f16):
+    # f16 = 2: also the layer-0 pre-pass in split fp16 (tuning dense_f16 = 2)
+    with tuning.override(chain_f16=int(f16 > 0), dense_f16=2 if f16 == 2 else 1):
         torch.manual_seed(900 + case)
         with torch.no_grad():
             newp, newf = sa(x.to(DEV), None if f is None else f.to(DEV))
@@ -381,13 +387,18 @@ DENSE_F16 = [
     (3, 64, 64, [64, 96, 128], 3, "tiny_row"),         # one layer-1 weight row 1e-6, var 1e-12
     (3, 64, 64, [64, 96, 128], 3, "cloud_1e4"),        # cloud 1's hidden values 1e4 x cloud 0's
     (3, 61, 64, [64, 128], 3, "K16"),                  # K = 16 points: split bf16 only
+    (3, 64, 64, [64, 96, 128], 3, "coords_1e3"),       # layer-0 xyz ~1e3 (its own scale)
+    (3, 64, 64, [64, 96, 128], 3, "feat_1e-5"),        # layer-0 features ~1e-5
+    (3, 61, 64, [64, 128], 3, "feat_odd"),             # D % 4 != 0: scalar row reads for the scale
 ]
 
 
-@pytest.mark.parametrize("f16", [1, 0])
+@pytest.mark.parametrize("f16", [2, 1, 0])
 @pytest.mark.parametrize("case", range(len(DENSE_F16)))
 def test_dense_split_f16_vs_oracle(case, f16):
-    """The fp32-accurate dense layers after the first run split fp16 by default: within a tenth
+    """The fp32-accurate dense layers run split fp16 by default (the first over points with the
+    scale of its own rows when a cloud fills whole 32-row blocks, the later ones with the maxima
+    their producer wrote): within a tenth
     of the 1e-5 tolerance of the float64 oracle, also at magnitudes outside fp16's range unless
     scaled; a cloud's scale never depends on the other clouds of the batch (cloud_1e4: cloud 0
     alone gives the same bits).  f16 = 0: tuning dense_f16 = 0 (split bf16)."""
@@ -400,6 +411,10 @@ def test_dense_split_f16_vs_oracle(case, f16):
     feat = torch.randn(B, N, D, generator=torch.Generator().manual_seed(1500 + case))
     if kind == "cloud_1e4":
         feat[1] *= 1e4
+    if kind == "coords_1e3":
+        pts *= 1e3
+    if kind == "feat_1e-5":
+        feat *= 1e-5
     torch.manual_seed(1600 + case)
     sa = pn2.PointNetSetAbstraction(None, None, None, C + D, mlp, True)
     cases.randomize_bn(sa, 1700 + case)
