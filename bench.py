@@ -537,7 +537,8 @@ def main():
                 "compulsory_bytes_per_launch": mlp["bytes"] / mlp["launches"],
                 "kernel": "%s (sa_chain_kernel / dense_split_kernel, %s)" % (
                     mlp_name, "bf16, 1 MFMA per product" if prec == "bf16" else
-                    "fp32-accurate split fp16 (chains) / split bf16 (dense layers)"),
+                    "fp32-accurate split fp16 (chains, dense hidden layers) / split bf16 (first dense "
+                    "layer, streamed chain inputs)"),
                 "fp32_mfma_peak": PEAK_F32_MFMA,
                 "frac_of_fp32_mfma_peak": round(achieved / PEAK_F32_MFMA, 4),
                 "flops_per_launch": mlp["flops"] / mlp["launches"],
@@ -582,8 +583,9 @@ def main():
             "scaling": "strong" if a.config in STRONG else "weak", "vs_baseline": None,
             "dtype": ("bf16 (MLP operands bf16, fp32 accumulate / BN / max; FPS/ball query f32)"
                       if prec == "bf16" else
-                      "f32 (MLP products fp32-accurate: split fp16 x3 in the chains, split bf16 x6 in "
-                      "the dense layers, fp32 accumulate; FPS/ball query f32)"),
+                      "f32 (MLP products fp32-accurate: split fp16 x3 in the chains and the dense "
+                      "hidden layers, split bf16 x6 in the first dense layers, fp32 accumulate; "
+                      "FPS/ball query f32)"),
             "data": "synthetic: seeded uniform clouds normalised to the unit sphere%s; seeded "
                     "random-init weights and BN statistics (eval mode)" % (
                         " + 7-way one-hot" if kind == "onehot10" else ""),
