@@ -202,6 +202,7 @@ FpsArgs pn2::fps_args(const float *pts, int64_t N, int64_t C, int64_t sb, int64_
     F.out_packed = out_packed;
     F.pts_packed = pts_packed;
     F.cp = (int)pn2_packed_stride(C);
+    F.prio = tuning().fps_prio ? 1 : 0;
     F.start = start;
     return F;
 }

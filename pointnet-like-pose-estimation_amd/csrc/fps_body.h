@@ -43,7 +43,8 @@ struct FpsArgs {
     int S;
     int64_t *out_idx;
     float *out_pts, *out_packed, *pts_packed;
-    int cp;  // pn2_packed_stride(C)
+    int cp;    // pn2_packed_stride(C)
+    int prio;  // raise the waves' issue priority (tuning fps_prio)
     FpsStart start;
 };
 
@@ -116,7 +117,7 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
     // In the pipelined launch FPS shares every SIMD with the MLP kernels' waves, and its
     // dependent chain (one short VALU burst, a reduction and a barrier per iteration) is the
     // pipeline's critical path: its waves take issue priority over co-resident waves.
-    __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
+    if (F.prio) __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
     constexpr int SLOT = (CM + 2 + 3) & ~3;  // {max, index, coords...} padded to 16 bytes
     const int C = FIXED ? CM : Crt;
     const int tid = threadIdx.x;

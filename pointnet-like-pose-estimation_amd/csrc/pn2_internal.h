@@ -41,6 +41,7 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(chain_prepass, 1)    /* 0: no layer-0 pre-pass (wide first layers of a chain)        */ \
     X(compact, 1)          /* 0: no compact neighbourhoods (every padded row computed)     */ \
     X(compact_pool, 16)     /* LDS pool rows of compact chain launches (0: automatic)       */ \
+    X(fps_prio, 1)         /* 1: FPS waves at raised issue priority (s_setprio 3)            */ \
     X(fps_side, 1)         /* 0: FPS side jobs as their own launches, not in the chain's    */ \
     X(compact_stages, 2)   /* weight-ring stages of compact chain launches (2 or 3)        */ \
     X(bq_waves, 16)        /* ball query waves per workgroup (8 or 16; 0: 16 for xyz clouds  */ \
