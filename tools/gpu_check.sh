@@ -31,7 +31,7 @@ for s in $STEPS; do
           rm -rf $OUT/pmc_${cfg}_$c
           timeout -k 10 300 rocprofv3 --pmc $c -d $OUT/pmc_${cfg}_$c -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timer --no-pipeline > $OUT/pmc_${cfg}_$c.log 2>&1; ok $? pmc_${cfg}_$c
         done
-        python tools/pmc_traffic.py $OUT/pmc_${cfg}_FETCH_SIZE $OUT/pmc_${cfg}_WRITE_SIZE --config $cfg > $OUT/pmc_summary_$cfg.txt 2>&1
+        python tools/pmc_traffic.py $OUT/pmc_${cfg}_FETCH_SIZE $OUT/pmc_${cfg}_WRITE_SIZE --config $cfg --forwards 7 > $OUT/pmc_summary_$cfg.txt 2>&1
         head -3 $OUT/pmc_summary_$cfg.txt
       done
       cp profiles/pmc_traffic.json $OUT/pmc_traffic.json ;;

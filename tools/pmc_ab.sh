@@ -17,6 +17,6 @@ for kv in "${VS[@]}"; do
     timeout -k 10 300 rocprofv3 --pmc $c -d $OUT/${tag}_$c -o run --output-format csv -- python3 bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timer --no-pipeline > $OUT/${tag}_$c.log 2>&1
     rc=$?; unset PN2_TUNING; [ $rc -ne 0 ] && { echo "pmc $tag $c rc=$rc"; tail -5 $OUT/${tag}_$c.log; exit $rc; }
   done
-  python3 tools/pmc_traffic.py $OUT/${tag}_FETCH_SIZE $OUT/${tag}_WRITE_SIZE --config $CFG --no-save > $OUT/summary_$tag.txt 2>&1
+  python3 tools/pmc_traffic.py $OUT/${tag}_FETCH_SIZE $OUT/${tag}_WRITE_SIZE --config $CFG --forwards 7 --no-save > $OUT/summary_$tag.txt 2>&1
   echo "== $tag ($tun)"; grep -E "sa_chain|compact_scan|u_table|dense_lds|dense_split|per_call" $OUT/summary_$tag.txt
 done

@@ -55,6 +55,10 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--config", default="ssg")
     ap.add_argument("--no-save", action="store_true", help="print only (A/B passes)")
+    ap.add_argument("--forwards", type=float, default=0.0,
+                    help="forwards the profiled run made (bench --steps + --warmup, eager); default: "
+                         "counted from the FPS launches (not valid where the next layer's FPS rides "
+                         "on the MLP launch, pn2_fps_side)")
     a = ap.parse_args()
     if a.config not in FPS_PER_FORWARD:
         raise SystemExit("pmc_traffic: no per-forward launch counts for config %r" % a.config)
@@ -70,7 +74,7 @@ def main():
         kernels[short(name)] = {"dispatches": max(len(f), len(w)), "fetch_bytes": fb,
                                 "write_bytes": wb}
     n_fps = sum(len(v) for k, v in fetch.items() if FORWARD_MARKER in k)
-    forwards = n_fps / FPS_PER_FORWARD[a.config]
+    forwards = a.forwards or n_fps / FPS_PER_FORWARD[a.config]
     for name, v in fetch.items():
         if any(k in name for k in MLP_KERNELS):
             mlp_total += 2 * 1024 * sum(v)
