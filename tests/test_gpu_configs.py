@@ -17,7 +17,8 @@ float64 MLP + max (pointnet2_utils.py:163-172, 211-221): fp32 within 1e-5 relati
 output's max magnitude; bf16 against the oracle's bf16 emulation within 2e-3 (test_gpu_bf16.py's
 bar).  Features are checked for every cloud where the float64 MLP takes seconds (msg, pose) and
 for 33 clouds spread over the batch at stress (every 4th and the last; the oracle's bf16
-emulation of all 128 takes minutes); indices for every cloud everywhere.  The same batch through pn2.pipeline.GraphedPipeline
+emulation of all 128 takes minutes) -- there every cloud's features are also checked against a
+torch restatement of the bf16 arithmetic on the GPU (same bar); indices for every cloud everywhere.  The same batch through pn2.pipeline.GraphedPipeline
 (geometry groups of 2 batches, graphs on their streams) must give the eager outputs bit for bit.
 """
 import itertools
@@ -111,6 +112,23 @@ def _mlp(grouped, layers, prec):
     return (oracle.mlp_max_bf16 if prec == "bf16" else oracle.mlp_max)(grouped, layers)
 
 
+def _torch_mlp_max_bf16(grouped, layers):
+    """The bf16 MLP + max restated in torch on the GPU (every clouds' check at STRESS, where the
+    oracle's emulation takes minutes): each layer's input and weight rounded to bf16, products
+    and sums in fp32 (exact products; only the fp32 summation order differs from the kernels'),
+    conv bias + eval BN folded as the kernels fold them, ReLU, max over the K rows.
+    grouped [B, S, K, Cin] float32 (device) -> [B, S, Cout] float64 (host)."""
+    x = grouped
+    for L in layers:
+        W = torch.from_numpy(L["W"]).to(x.device)
+        alpha = torch.from_numpy(L["gamma"] / np.sqrt(L["var"].astype(np.float64) + L["eps"])).float()
+        beta = (alpha.double() * (torch.from_numpy(L["b"]).double() - torch.from_numpy(L["mean"]).double())
+                + torch.from_numpy(L["beta"]).double()).float()
+        y = x.to(torch.bfloat16).float() @ W.to(torch.bfloat16).float().t()
+        x = torch.relu(y * alpha.to(x.device) + beta.to(x.device))
+    return x.max(dim=2)[0].double().cpu().numpy()
+
+
 def _check_layer(mod, p_in, f_in, p_out, f_out, start, check, prec, what):
     from pn2.pointnet2_utils import PointNetSetAbstractionMsg
     pts = p_in.permute(0, 2, 1).numpy()            # [B, N, C] with the module's strides
@@ -118,6 +136,7 @@ def _check_layer(mod, p_in, f_in, p_out, f_out, start, check, prec, what):
     got = f_out.permute(0, 2, 1).numpy()           # [B, S, Cout]
     rtol = 2e-3 if prec == "bf16" else 1e-5
     check = list(check)
+    full = prec == "bf16" and len(check) < pts.shape[0]  # every cloud through the torch restatement
     if getattr(mod, "group_all", False):
         rows = pts if feat is None else np.concatenate([pts, feat], -1)
         layers = _layers(mod.mlp_convs, mod.mlp_bns)
@@ -125,6 +144,9 @@ def _check_layer(mod, p_in, f_in, p_out, f_out, start, check, prec, what):
             cl = check[c0:c0 + 8]
             want = _mlp(rows[cl][:, None], layers, prec)
             _close(got[cl], want, rtol, what + " group_all features")
+        if full:
+            want = _torch_mlp_max_bf16(torch.from_numpy(np.ascontiguousarray(rows)).to(DEV)[:, None], layers)
+            _close(got, want, rtol, what + " group_all features, every cloud (torch bf16)")
         assert float(np.abs(p_out.numpy()).max()) == 0.0
         return
     S = mod.point_number
@@ -149,6 +171,15 @@ def _check_layer(mod, p_in, f_in, p_out, f_out, start, check, prec, what):
                                    feature_first=ff)
             _close(got[cl, :, col:col + cout], _mlp(grouped, layers, prec), rtol,
                    "%s r=%g K=%d features, clouds %s" % (what, r, K, cl[:3]))
+        if full:
+            for c0 in range(0, pts.shape[0], 32):
+                cl = list(range(c0, min(c0 + 32, pts.shape[0])))
+                grouped = oracle.group(pts[cl], None if feat is None else feat[cl], idx[cl], ctr[cl],
+                                       feature_first=ff)
+                want = _torch_mlp_max_bf16(torch.from_numpy(np.ascontiguousarray(grouped, np.float32)).to(DEV),
+                                           layers)
+                _close(got[cl, :, col:col + cout], want, rtol,
+                       "%s r=%g K=%d features, clouds %d.. (torch bf16)" % (what, r, K, c0))
         col += cout
     assert col == got.shape[2]
 
