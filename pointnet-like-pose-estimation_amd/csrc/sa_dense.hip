@@ -96,7 +96,20 @@ struct DenseSplitArgs {
     // out_max [M/32][tiles] (or null): this layer's own per-(row block, tile) max |value| bits of
     // the rows it writes (pool == 0), for an NP = 2 layer after it
     unsigned *out_max;
+    // fragment-ordered hidden rows (frag_off): the producing layer writes them (frag_out), the
+    // register-staged consumer reads each lane's k-block as 32 contiguous bytes (frag_in, rows
+    // mode: `rows` is the block array, rs unused) -- a wave's A operand one 2 KB run per k-block
+    // instead of 16-byte pieces of 32 rows
+    int frag_in, frag_out;
 };
+
+// Fragment order of a [M][16*kbw] row matrix: block (32-row block, 16-channel k-block) = 512
+// floats, lane (r, h) = (row & 31) + 32h holding channels (j&3) + 8(j>>2) + 4h of its row in
+// element j -- the A-fragment order of split_bf16.h, so a lane's 8 values are contiguous
+__host__ __device__ __forceinline__ int64_t frag_off(int64_t row, int col, int kbw) {
+    return (((row >> 5) * kbw + (col >> 4)) * 64 + (row & 31) + 32 * ((col >> 2) & 1)) * 8 + (col & 3) +
+           4 * ((col >> 3) & 1);
+}
 
 // NP = 2: this wave's activation scale, from the max |value| of its 32 rows (rb*32 ..): the
 // producing layer's per-(row block, tile) maxima (in_max, rows mode), or -- a first layer over
@@ -224,7 +237,12 @@ void dense_split_kernel(const DenseSplitArgs A) {
     const ActScale asc = dense_act_scale<NP>(A, (row0 >> 5) + wave, lane);
     const float *arow = nullptr, *frow = nullptr, *prow = nullptr;
     if (A.mode == 0) {
-        arow = A.rows + (int64_t)(valid ? R : 0) * A.rs;
+        if (A.frag_in) {  // this lane's 8 values of k-block 0 (rows past M: the last row's)
+            const int fr = valid ? R : A.M - 1;
+            arow = A.rows + ((int64_t)(fr >> 5) * A.kb * 64 + (fr & 31) + 32 * h) * 8;
+        } else {
+            arow = A.rows + (int64_t)(valid ? R : 0) * A.rs;
+        }
     } else {
         const int b = (valid ? R : 0) / A.N, n = (valid ? R : 0) - b * A.N;
         prow = A.pts + (int64_t)b * A.pb + (int64_t)n * A.pn;
@@ -242,6 +260,16 @@ void dense_split_kernel(const DenseSplitArgs A) {
             for (int j = 0; j < 8; ++j) {
                 const int ch = (j & 3) + 8 * (j >> 2) + 4 * h;
                 x[j] = ch < A.C ? prow[(int64_t)ch * A.pc] : 0.f;
+            }
+            return;
+        }
+        if (A.mode == 0 && A.frag_in) {
+            const float *p = arow + 512 * (int64_t)kb;
+#pragma unroll
+            for (int run = 0; run < 2; ++run) {
+                const cfloatx4 q = *reinterpret_cast<const cfloatx4 *>(p + 4 * run);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[4 * run + i] = q[i];
             }
             return;
         }
@@ -267,9 +295,22 @@ void dense_split_kernel(const DenseSplitArgs A) {
     // lrow + 16 kb (rows mode: the row; group_all: the features, blocks >= 1) -- two 16-byte
     // loads at immediate offsets from one pointer per stage, no per-element branches
     const float *lrow = A.mode == 0 ? arow : frow - 16;
-    lrow += 4 * h;
+    if (!(A.mode == 0 && A.frag_in)) lrow += 4 * h;
     auto load_fast = [&](int c, float (&x)[kKC][8]) {
         const int kb0 = c * kKC;
+        if (A.mode == 0 && A.frag_in) {  // k-block kb: 8 contiguous floats at lrow + 512 kb
+#pragma unroll
+            for (int k = 0; k < kKC; ++k) {
+                const float *p = lrow + 512 * (int64_t)min(kb0 + k, A.kb - 1);
+#pragma unroll
+                for (int run = 0; run < 2; ++run) {
+                    const cfloatx4 q = *reinterpret_cast<const cfloatx4 *>(p + 4 * run);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[k][4 * run + i] = q[i];
+                }
+            }
+            return;
+        }
         if (kb0 + kKC <= A.kb) {
             const float *p = lrow + 16 * kb0;
             constexpr int ks = 16, rs_ = 8;
@@ -395,7 +436,7 @@ void dense_split_kernel(const DenseSplitArgs A) {
                 if (row < A.M) {
                     const float y = __builtin_fmaf(acc[i][q], al, be);
                     const float v = A.raw ? acc[i][q] * al : (A.norelu ? y : chain_relu(y));
-                    A.out[(int64_t)row * A.ostride + col] = v;
+                    A.out[A.frag_out ? frag_off(row, col, 2 * A.tiles) : (int64_t)row * A.ostride + col] = v;
                     tmax = max(tmax, __float_as_uint(v) & 0x7FFFFFFFu);
                 }
             }
@@ -773,7 +814,7 @@ void dense_lds_kernel(const DenseSplitArgs A) {
                 if (row < A.M) {
                     const float y = __builtin_fmaf(acc[i][q], al, be);
                     const float v = A.raw ? acc[i][q] * al : (A.norelu ? y : chain_relu(y));
-                    A.out[(int64_t)row * A.ostride + col] = v;
+                    A.out[A.frag_out ? frag_off(row, col, 2 * A.tiles) : (int64_t)row * A.ostride + col] = v;
                     tmax = max(tmax, __float_as_uint(v) & 0x7FFFFFFFu);
                 }
             }
@@ -1017,7 +1058,8 @@ int dense_last_planes() { return g_dense_planes; }
 // Workspace of the layer-by-layer path: two [M][w] fp32 halves, then two [ceil(M/32)][w/32]
 // uint max tables (the split-fp16 layers' activation scales, split_bf16.h)
 int64_t dense_split_ws_bytes(int64_t M, int64_t w) {
-    return 2 * M * w * 4 + 2 * ((M + 31) / 32) * ((w + 31) / 32) * 4;
+    const int64_t Mp = (M + 31) / 32 * 32;  // fragment-ordered halves cover whole row blocks
+    return 2 * Mp * w * 4 + 2 * (Mp / 32) * ((w + 31) / 32) * 4;
 }
 
 // Widest hidden layer of a chain the split dense path runs layer by layer (0: not eligible).
@@ -1047,8 +1089,8 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
     // must start at a 32-row block (K % 32 == 0) so its scale never depends on other clouds.
     // Tuning dense_f16 = 0: split bf16 everywhere.
     const bool f16 = np == 3 && tuning().dense_f16 && K % 32 == 0;
-    const int64_t tw = (w + 31) / 32, nrb = (M + 31) / 32;
-    unsigned *maxtab = nlayers > 1 ? reinterpret_cast<unsigned *>(ws + 2 * M * w) : nullptr;
+    const int64_t tw = (w + 31) / 32, nrb = (M + 31) / 32, Mp = nrb * 32;
+    unsigned *maxtab = nlayers > 1 ? reinterpret_cast<unsigned *>(ws + 2 * Mp * w) : nullptr;
     // the first layer over points (group_all) takes its scale from its own rows when a cloud's
     // points fill whole 32-row blocks
     const bool f16_first = f16 && tuning().dense_f16 >= 2 && s.mode == PN2_SRC_GROUP_ALL && s.N % 32 == 0;
@@ -1071,7 +1113,7 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
                 A.rows = s.rows;
                 A.rs = s.rs;
             } else {
-                A.rows = ws + ((l - 1) & 1) * M * w;
+                A.rows = ws + ((l - 1) & 1) * Mp * w;
                 A.rs = w;
             }
             A.cin = (int)layers[l].cin;
@@ -1095,13 +1137,23 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
         A.pool = last ? pool : 0;
         A.norelu = (layers[l].flags & PN2_LAYER_NO_RELU) ? 1 : 0;
         A.K = (int)K;
-        A.out = last ? out : ws + (l & 1) * M * w;
+        A.out = last ? out : ws + (l & 1) * Mp * w;
         A.ostride = last ? ostride : w;
+        return A;
+    };
+    // hidden rows in fragment order where their consumer is the register-staged kernel (the
+    // LDS-staged one DMAs whole row lines); tuning dense_frag = 0: row-major everywhere
+    bool frag[5] = {false, false, false, false, false};
+    for (int l = 1; l < nlayers && l < 5; ++l) frag[l] = tuning().dense_frag && dense_lds_tile(make(l)) == 0;
+    auto make_f = [&](int l) {
+        DenseSplitArgs A = make(l);
+        if (l >= 1 && frag[l]) A.frag_in = 1, A.vec = 1;
+        if (l + 1 < nlayers && l + 1 < 5 && frag[l + 1]) A.frag_out = 1;
         return A;
     };
     // a last layer that pools by HBM atomics gets its output zeroed by the layer before it
     // (one launch fewer than a memset: PointNet-v1's max over N points, group_all over K > 256)
-    DenseSplitArgs last = make(nlayers - 1);
+    DenseSplitArgs last = make_f(nlayers - 1);
     const bool fold_zero = nlayers > 1 && last.pool && dense_needs_zero(last, layer_np(nlayers - 1));
     if (s.zero_out && s.zero_count > 0) {  // the caller's side job rides on the last layer
         last.zero = s.zero_out;
@@ -1112,7 +1164,7 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
     int64_t flops[4] = {0, 0, 0, 0};
     for (int l = 0; l < nlayers; ++l) {
         flops[layer_np(l)] += layers[l].cin * layers[l].cout;
-        DenseSplitArgs A = l == nlayers - 1 ? last : make(l);
+        DenseSplitArgs A = l == nlayers - 1 ? last : make_f(l);
         if (fold_zero && l == nlayers - 2) {
             A.zero = last.out;
             A.zrows = last.M / last.K;

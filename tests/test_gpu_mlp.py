@@ -274,6 +274,30 @@ def test_dense_lds_matches_register_staged(case, prec):
         _close(outs[0].transpose(0, 2, 1), want)
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", range(len(DENSE_LDS)))
+def test_dense_frag_rows_bit_identical(case, prec):
+    """Hidden rows in MFMA-fragment order (tuning dense_frag = 1, the register-staged kernel's
+    default) vs row-major: the same values in another layout -- the same bits, fp32 and bf16,
+    including partial 32-row blocks (B = 5 / 3 clouds)."""
+    import pn2
+    from pn2 import tuning
+    C, D, N, mlp, B = DENSE_LDS[case]
+    pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 900 + case)
+    feat = torch.randn(B, N, D, generator=torch.Generator().manual_seed(910 + case))
+    torch.manual_seed(case)
+    sa = pn2.PointNetSetAbstraction(None, None, None, C + D, mlp, True)
+    cases.randomize_bn(sa, case)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous().to(DEV)
+    f = feat.permute(0, 2, 1).contiguous().to(DEV)
+    outs = []
+    for frag in (1, 0):
+        with torch.no_grad(), pn2.mlp_precision(prec), tuning.override(dense_lds=0, dense_frag=frag):
+            outs.append(sa(x, f)[1].cpu().numpy())
+    np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
 def test_dense_lds_rows_source_v1():
     """PointNet-v1 encoder MLPs (rows source, unpooled and max over N = 1024 points, the last
     layer signed / without ReLU): LDS-staged == register-staged bits."""
