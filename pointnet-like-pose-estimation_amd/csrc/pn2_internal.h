@@ -58,6 +58,7 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(dense_minwg, 256)    /* workgroups a wider dense tile must still leave                 */ \
     X(dense_wide_minwg, 512) /* workgroups the 256 x 128 dense tile must leave              */ \
     X(dense_lds, 1)        /* 1: LDS-staged dense kernel for layers of >= dense_lds_mincin   */ \
+                           /* (2: only first layers over points, group_all / pre-pass)      */ \
                            /* input channels (faster alone: the eager forward; the          */ \
                            /* pipelines run with 0, pn2/tuning.py PIPELINE_PROFILE)         */ \
     X(dense_lds_mincin, 0)                                                                     \

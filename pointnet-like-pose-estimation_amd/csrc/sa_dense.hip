@@ -866,6 +866,7 @@ static const int kLdsTiles[] = {82, 44, 42, 22};
 
 static int dense_lds_tile(const DenseSplitArgs &A) {
     if (!tuning().dense_lds || !A.vec) return 0;
+    if (tuning().dense_lds == 2 && A.mode == 0) return 0;  // 2: group_all / pre-pass layers only
     // tuning dense_lds_mincin keeps narrower layers on the register-staged kernel (default 0:
     // none -- SSG eager 67.6k at 0 or 128 vs 66.6k at 256, PointNet-v1 equal or faster,
     // tools/gpu_r04af.sh)
