@@ -20,6 +20,7 @@
  *   pn2_fps_f32            farthest_point_sample            model/pointnet2_utils.py:47-68
  *   pn2_fps_ws_f32         the same, any N (workspace)       model/pointnet2_utils.py:47-68
  *   pn2_fps_host_ws_f32    the same, start drawn on the host model/pointnet2_utils.py:59
+ *   pn2_ball_query_multi_i32  query_ball_point per MSG radius   model/pointnet2_utils.py:197-203
  *                          (+ index_points(points, fps_idx)  model/pointnet2_utils.py:106)
  *   pn2_ball_query_f32     query_ball_point + square_distance model/pointnet2_utils.py:70-90, 5-26
  *   pn2_pack_points_f32    torch.sum(points**2,-1) of square_distance model/pointnet2_utils.py:24-25
@@ -166,6 +167,14 @@ int pn2_ball_query_cnt_f32(const float *pts_packed, const float *ctr_packed, int
 int pn2_ball_query_i32(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N,
                        int64_t S, int64_t C, double radius, int64_t K, int32_t *out_idx,
                        int32_t *out_cnt, void *stream);
+/* nr (1..3) radii of one centroid set in one launch -- the scales of an MSG layer
+ * (pointnet2_utils.py:197-203 calls query_ball_point once per radius): each pair's distance
+ * computed once and tested against every radius; out_idx[r] [B,S,K[r]] int32 and out_cnt[r]
+ * [B,S] (or out_cnt / out_cnt[r] NULL) exactly as nr pn2_ball_query_i32 calls would write them. */
+int pn2_ball_query_multi_i32(const float *pts_packed, const float *ctr_packed, int64_t B,
+                             int64_t N, int64_t S, int64_t C, int nr, const double *radii,
+                             const int64_t *K, int32_t *const *out_idx, int32_t *const *out_cnt,
+                             void *stream);
 
 /* square_distance(src, dst) -> out [B,S,N] float32 from packed records of src [B,S,cp] and
  * dst [B,N,cp] (same float32 recipe as the ball query). */

@@ -33,6 +33,7 @@
 // (uniform s_load_dwordx16, no staging) measured slower (11-13 us): SMEM returns out of order,
 // so every use waits for all loads in flight and their latency is exposed.
 #include <stdlib.h>
+#include <string.h>
 
 #include "pn2_internal.h"
 
@@ -70,25 +71,38 @@ __device__ __forceinline__ void bq_insert(unsigned &wd, float d, float r2) {
 
 // OT: the index type written (int64: the reference's query_ball_point; int32: the SA path's
 // lists, half the bytes).  ROWBUF: each lane's hits go to its centroid's row of an LDS buffer
-// (64 rows of K + 1 entries, dynamic LDS); after the scan every row is written out whole,
-// padding included, one coalesced row per wave step.  !ROWBUF (rows too long for LDS, any
+// (64 rows of K + 1 entries per radius, dynamic LDS); after the scan every row is written out
+// whole, padding included, one coalesced row per wave step.  !ROWBUF (rows too long for LDS, any
 // K <= N as the reference's slice [:, :, :nsample] allows, pointnet2_utils.py:87): a hit goes
 // straight to its slot of the output row (the slot is known from the prefix), the row's first
 // hit is kept in LDS for the padding, and only the padding is written in the coalesced pass.
-template <int CP, int CC, int NW, int P, typename OT, bool ROWBUF>
+// NR radii (the MSG layers' scales, pointnet2_utils.py:197-203): one distance per (centroid,
+// point) pair, compared with each radius -- NR independent queries, each exactly the
+// one-radius query's result (hits past a radius' K are dropped; the scan stops once every
+// radius of every centroid has its K).
+constexpr int kBqMaxR = 3;
+template <typename OT>
+struct BqOut {
+    float r2[kBqMaxR];
+    int K[kBqMaxR];
+    int obase[kBqMaxR];  // ROWBUF: element offset of radius r's [64][K + 1] rows in the LDS buffer
+    OT *out[kBqMaxR];
+    int *cnt[kBqMaxR];
+};
+
+template <int CP, int CC, int NW, int P, typename OT, bool ROWBUF, int NR>
 __global__ __launch_bounds__(64 * P) void ball_query_kernel(
-    const float *__restrict__ pts, const float *__restrict__ ctr, int N, int S, int C_, float r2,
-    int K, int small_, OT *__restrict__ out, int *__restrict__ out_cnt, unsigned *__restrict__ err) {
+    const float *__restrict__ pts, const float *__restrict__ ctr, int N, int S, int C_, int small_,
+    const BqOut<OT> O, unsigned *__restrict__ err) {
     constexpr int TS = 32 * NW;
     constexpr int TV = P * TS * CP / 4;  // float4 per staged round
     __shared__ float4 tile[TV];
     const int C = CC > 0 ? CC : C_;
     const bool small = CC > 0 ? false : small_;  // the specialised instances never see tiny shapes
-    __shared__ int cnts[2][P][64];
-    __shared__ int first[64];  // !ROWBUF: each row's first hit (slot 0)
+    __shared__ int cnts[2][NR][P][64];
+    __shared__ int first[NR][64];  // !ROWBUF: each row's first hit (slot 0)
     extern __shared__ __attribute__((aligned(16))) char bq_dyn[];
-    OT *obuf = reinterpret_cast<OT *>(bq_dyn);  // [64][K + 1]
-    const int KP = K + 1;
+    OT *obuf = reinterpret_cast<OT *>(bq_dyn);  // [NR][64][K + 1]
 
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -126,12 +140,16 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
         }
     };
 
-    int total = valid ? 0 : K;  // hits so far (invalid lanes count as done)
+    int total[NR];  // hits so far per radius (invalid lanes count as done)
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) total[rr] = valid ? 0 : O.K[rr];
     int r = 0;
     for (int R0 = 0; R0 < N; R0 += P * TS, ++r) {
         const int seg0 = R0 + w * TS;
-        unsigned bits[NW];
-        int mine = 0;
+        unsigned bits[NR][NW];
+        int mine[NR];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) mine[rr] = 0;
         {  // stage the round's P*TS records (coalesced 16-byte loads by the whole workgroup)
             if (R0 > 0) __syncthreads();  // every wave is done with the previous round's tile
             const int npt = min(P * TS, N - R0);
@@ -144,7 +162,9 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
         for (int t = 0; t < NW; ++t) {
             const int base = seg0 + 32 * t;
             const int np = min(32, N - base);  // points in this word (<= 0: none)
-            unsigned wd = 0;
+            unsigned wd[NR];
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr) wd[rr] = 0;
             if (np == 32) {
 #pragma unroll 8
                 for (int i = 0; i < 32; ++i) {
@@ -155,71 +175,88 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
                         const float4 q4 = tp[v];
                         pv[4 * v] = q4.x; pv[4 * v + 1] = q4.y; pv[4 * v + 2] = q4.z; pv[4 * v + 3] = q4.w;
                     }
-                    bq_insert(wd, bq_dist<CP>(c, ssq_c, pv, C, small), r2);  // point base+i -> bit 31-i
+                    const float d = bq_dist<CP>(c, ssq_c, pv, C, small);
+#pragma unroll
+                    for (int rr = 0; rr < NR; ++rr) bq_insert(wd[rr], d, O.r2[rr]);  // point base+i -> bit 31-i
                 }
             } else if (np > 0) {
                 for (int i = 0; i < 32; ++i) {
-                    unsigned h = 0;
+                    float d = 0.f;
                     if (i < np) {
                         float pv[CP];
                         point_rec(w * TS + 32 * t + i, pv);
-                        h = bq_near<CP>(c, ssq_c, pv, C, small, r2);
+                        d = bq_dist<CP>(c, ssq_c, pv, C, small);
                     }
-                    wd = (wd << 1) | h;
+#pragma unroll
+                    for (int rr = 0; rr < NR; ++rr) wd[rr] = (wd[rr] << 1) | (i < np ? (unsigned)!(d > O.r2[rr]) : 0u);
                 }
             }
-            bits[t] = wd;
-            mine += __builtin_popcount(wd);
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr) {
+                bits[rr][t] = wd[rr];
+                mine[rr] += __builtin_popcount(wd[rr]);
+            }
         }
-        cnts[r & 1][w][lane] = mine;
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) cnts[r & 1][rr][w][lane] = mine[rr];
         __syncthreads();
-        int off = total, round = 0;
+        bool more = false;
 #pragma unroll
-        for (int v = 0; v < P; ++v) {
-            const int x = cnts[r & 1][v][lane];
-            if (v < w) off += x;
-            round += x;
-        }
-        // this segment's hits, in index order, into the slots [off, K)
-        OT *orow = out + q * K;  // !ROWBUF (invalid lanes start at total = K: no writes)
+        for (int rr = 0; rr < NR; ++rr) {
+            const int K = O.K[rr];
+            int off = total[rr], round = 0;
 #pragma unroll
-        for (int t = 0; t < NW; ++t) {
-            unsigned wd = bits[t];
-            while (wd != 0 && off < K) {
-                const int i = __builtin_clz(wd);
-                const int n = seg0 + 32 * t + i;
-                if constexpr (ROWBUF) {
-                    obuf[lane * KP + off] = (OT)n;
-                } else {
-                    orow[off] = (OT)n;
-                    if (off == 0) first[lane] = n;
-                }
-                ++off;
-                wd ^= 0x80000000u >> i;
+            for (int v = 0; v < P; ++v) {
+                const int x = cnts[r & 1][rr][v][lane];
+                if (v < w) off += x;
+                round += x;
             }
+            // this segment's hits, in index order, into the slots [off, K)
+            OT *orow = O.out[rr] + q * K;  // !ROWBUF (invalid lanes start at total = K: no writes)
+#pragma unroll
+            for (int t = 0; t < NW; ++t) {
+                unsigned wd = bits[rr][t];
+                while (wd != 0 && off < K) {
+                    const int i = __builtin_clz(wd);
+                    const int n = seg0 + 32 * t + i;
+                    if constexpr (ROWBUF) {
+                        obuf[O.obase[rr] + lane * (K + 1) + off] = (OT)n;
+                    } else {
+                        orow[off] = (OT)n;
+                        if (off == 0) first[rr][lane] = n;
+                    }
+                    ++off;
+                    wd ^= 0x80000000u >> i;
+                }
+            }
+            total[rr] += round;
+            more = more || total[rr] < K;
         }
-        total += round;
-        if (__builtin_amdgcn_ballot_w64(total < K) == 0) break;  // same in every wave
+        if (__builtin_amdgcn_ballot_w64(more) == 0) break;  // same in every wave
     }
     __syncthreads();  // every row's hits are in obuf
 
     // rows out, hits then padding (the first hit; N when there is none: the reference's
     // pad), one centroid row per step, coalesced over the K slots; and the counts
-    for (int j = w; j < 64; j += P) {
-        if (g0 + j >= S) break;
-        const int cj = min(__builtin_amdgcn_readlane(total, j), K);
-        const OT fj = cj > 0 ? (ROWBUF ? obuf[j * KP] : (OT)first[j]) : (OT)N;
-        // no point within the radius: the row is padded with index N (the reference's
-        // out-of-range pad, pointnet2_utils.py:85-89, which makes its index_points raise
-        // IndexError); the SA kernels clamp such indices instead of reading past the cloud
-        if (cj == 0 && lane == 0) atomicOr(err, (unsigned)PN2_DEVERR_NO_NEIGHBOUR);
-        OT *o = out + ((int64_t)b * S + g0 + j) * K;
-        if constexpr (ROWBUF) {
-            for (int k = lane; k < K; k += 64) o[k] = k < cj ? obuf[j * KP + k] : fj;
-        } else {
-            for (int k = cj + lane; k < K; k += 64) o[k] = fj;  // the hits are already out
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+        const int K = O.K[rr], KP = K + 1;
+        for (int j = w; j < 64; j += P) {
+            if (g0 + j >= S) break;
+            const int cj = min(__builtin_amdgcn_readlane(total[rr], j), K);
+            const OT fj = cj > 0 ? (ROWBUF ? obuf[O.obase[rr] + j * KP] : (OT)first[rr][j]) : (OT)N;
+            // no point within the radius: the row is padded with index N (the reference's
+            // out-of-range pad, pointnet2_utils.py:85-89, which makes its index_points raise
+            // IndexError); the SA kernels clamp such indices instead of reading past the cloud
+            if (cj == 0 && lane == 0) atomicOr(err, (unsigned)PN2_DEVERR_NO_NEIGHBOUR);
+            OT *o = O.out[rr] + ((int64_t)b * S + g0 + j) * K;
+            if constexpr (ROWBUF) {
+                for (int k = lane; k < K; k += 64) o[k] = k < cj ? obuf[O.obase[rr] + j * KP + k] : fj;
+            } else {
+                for (int k = cj + lane; k < K; k += 64) o[k] = fj;  // the hits are already out
+            }
+            if (O.cnt[rr] && lane == 0) O.cnt[rr][(int64_t)b * S + g0 + j] = cj;
         }
-        if (out_cnt && lane == 0) out_cnt[(int64_t)b * S + g0 + j] = cj;
     }
 }
 
@@ -227,9 +264,9 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
 
 using namespace pn2;
 
-template <int CP, int CC, typename OT>
+template <int CP, int CC, typename OT, int NR>
 static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, int64_t S,
-                     int64_t C, float r2, int64_t K, OT *out, int *cnt, hipStream_t st) {
+                     int64_t C, BqOut<OT> O, hipStream_t st) {
     const int64_t nblk = B * ((S + 63) / 64);
     PN2_REQUIRE(nblk < (int64_t)1 << 31, "pn2_ball_query_f32: too many centroids");
     // waves per workgroup: bq_waves = 16 (the default: alone on the chip more segments in
@@ -242,9 +279,13 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
     int nw = per_wave <= 32 ? 1 : per_wave <= 64 ? 2 : 4;
     if (CP > 4 && nw > 2) nw = 2;
     const int sm = (int)(S * N * C < 400);
-    // rows in an LDS buffer while it stays within bq_rowbuf_kb (<= 96 KB: with the tile and
+    // rows in an LDS buffer while they stay within bq_rowbuf_kb (<= 96 KB: with the tile and
     // the counts that still fits a CU), else hits straight to HBM
-    const size_t obytes = (size_t)64 * (K + 1) * sizeof(OT);
+    size_t obytes = 0;
+    for (int r = 0; r < NR; ++r) {
+        O.obase[r] = (int)(obytes / sizeof(OT));
+        obytes += (size_t)64 * (O.K[r] + 1) * sizeof(OT);
+    }
     const int64_t rb_kb = tuning().bq_rowbuf_kb < 96 ? tuning().bq_rowbuf_kb : 96;
     const bool rowbuf = obytes <= (size_t)rb_kb * 1024;
     unsigned *err = error_word();
@@ -252,12 +293,12 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
 #define PN2_BQ_L2(NW, PP, RB)                                                                          \
     do {                                                                                               \
         static const hipError_t attr = hipFuncSetAttribute(                                           \
-            reinterpret_cast<const void *>(&ball_query_kernel<CP, CC, NW, PP, OT, RB>),               \
+            reinterpret_cast<const void *>(&ball_query_kernel<CP, CC, NW, PP, OT, RB, NR>),           \
             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);                                   \
         PN2_REQUIRE(attr == hipSuccess, "pn2_ball_query_f32: LDS attribute");                         \
-        hipLaunchKernelGGL((ball_query_kernel<CP, CC, NW, PP, OT, RB>), dim3((unsigned)nblk),        \
-                           dim3(64 * PP), RB ? obytes : 0, st, pp, cp_, (int)N, (int)S, (int)C, r2,   \
-                           (int)K, sm, out, cnt, err);                                                 \
+        hipLaunchKernelGGL((ball_query_kernel<CP, CC, NW, PP, OT, RB, NR>), dim3((unsigned)nblk),    \
+                           dim3(64 * PP), RB ? obytes : 0, st, pp, cp_, (int)N, (int)S, (int)C, sm,   \
+                           O, err);                                                                    \
     } while (0)
 #define PN2_BQ_L(NW, PP)                    \
     do {                                    \
@@ -286,24 +327,38 @@ extern "C" int pn2_ball_query_f32(const float *pts_packed, const float *ctr_pack
                                   stream);
 }
 
+// nr radii over the same points and centroids (one launch; nr = 1: query_ball_point)
 template <typename OT>
 static int ball_query_impl(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N, int64_t S,
-                           int64_t C, double radius, int64_t K, OT *out_idx, int32_t *out_cnt, void *stream) {
-    PN2_REQUIRE(pts_packed && ctr_packed && out_idx, "pn2_ball_query_f32: null pointer");
-    PN2_REQUIRE(B >= 0 && N >= 1 && S >= 0 && C >= 1 && C <= kMaxC && K >= 1,
-                "pn2_ball_query_f32: bad shape B=%lld N=%lld S=%lld C=%lld K=%lld", (long long)B,
-                (long long)N, (long long)S, (long long)C, (long long)K);
-    PN2_REQUIRE(K <= N, "pn2_ball_query_f32: sample_number %lld > N %lld", (long long)K,
-                (long long)N);
+                           int64_t C, int nr, const double *radius, const int64_t *Ks, OT *const *out_idx,
+                           int32_t *const *out_cnt, void *stream) {
+    PN2_REQUIRE(pts_packed && ctr_packed && out_idx && radius && Ks, "pn2_ball_query_f32: null pointer");
+    PN2_REQUIRE(nr >= 1 && nr <= kBqMaxR, "pn2_ball_query_multi: 1..%d radii (got %d)", kBqMaxR, nr);
+    PN2_REQUIRE(B >= 0 && N >= 1 && S >= 0 && C >= 1 && C <= kMaxC,
+                "pn2_ball_query_f32: bad shape B=%lld N=%lld S=%lld C=%lld", (long long)B,
+                (long long)N, (long long)S, (long long)C);
+    BqOut<OT> O;
+    memset(&O, 0, sizeof(O));
+    for (int r = 0; r < nr; ++r) {
+        const int64_t K = Ks[r];
+        PN2_REQUIRE(out_idx[r], "pn2_ball_query_f32: null pointer");
+        PN2_REQUIRE(K >= 1, "pn2_ball_query_f32: bad shape K=%lld", (long long)K);
+        PN2_REQUIRE(K <= N, "pn2_ball_query_f32: sample_number %lld > N %lld", (long long)K, (long long)N);
+        // radius ** 2 in double (Python float), compared in float32 like torch's wrapped scalar
+        O.r2[r] = (float)(radius[r] * radius[r]);
+        O.K[r] = (int)K;
+        O.out[r] = out_idx[r];
+        O.cnt[r] = out_cnt ? out_cnt[r] : nullptr;
+    }
     PN2_REQUIRE(N < (int64_t)1 << 30 && S < (int64_t)1 << 30, "pn2_ball_query_f32: N or S too large");
     if (B == 0 || S == 0) return PN2_OK;
-    // radius ** 2 in double (Python float), compared in float32 like torch's wrapped scalar
-    const float r2 = (float)(radius * radius);
     hipStream_t st = as_stream(stream);
     const int64_t cp = pn2_packed_stride(C);
-#define PN2_BQ(CPV, CC) \
-    if (cp == CPV && (CC == 0 || (C == CC && S * N * C >= 400))) \
-        return launch_bq<CPV, CC, OT>(pts_packed, ctr_packed, B, N, S, C, r2, K, out_idx, out_cnt, st);
+#define PN2_BQ(CPV, CC)                                                                               \
+    if (cp == CPV && (CC == 0 || (C == CC && S * N * C >= 400)))                                      \
+        return nr == 1 ? launch_bq<CPV, CC, OT, 1>(pts_packed, ctr_packed, B, N, S, C, O, st)         \
+             : nr == 2 ? launch_bq<CPV, CC, OT, 2>(pts_packed, ctr_packed, B, N, S, C, O, st)         \
+                       : launch_bq<CPV, CC, OT, 3>(pts_packed, ctr_packed, B, N, S, C, O, st);
     PN2_BQ(4, 3) PN2_BQ(12, 10)
     PN2_BQ(4, 0) PN2_BQ(8, 0) PN2_BQ(12, 0) PN2_BQ(16, 0) PN2_BQ(20, 0)
 #undef PN2_BQ
@@ -313,13 +368,23 @@ static int ball_query_impl(const float *pts_packed, const float *ctr_packed, int
 extern "C" int pn2_ball_query_cnt_f32(const float *pts_packed, const float *ctr_packed, int64_t B,
                                       int64_t N, int64_t S, int64_t C, double radius, int64_t K,
                                       int64_t *out_idx, int32_t *out_cnt, void *stream) {
-    return ball_query_impl<int64_t>(pts_packed, ctr_packed, B, N, S, C, radius, K, out_idx, out_cnt, stream);
+    return ball_query_impl<int64_t>(pts_packed, ctr_packed, B, N, S, C, 1, &radius, &K, &out_idx,
+                                    out_cnt ? &out_cnt : nullptr, stream);
 }
 
 extern "C" int pn2_ball_query_i32(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N,
                                   int64_t S, int64_t C, double radius, int64_t K, int32_t *out_idx,
                                   int32_t *out_cnt, void *stream) {
-    return ball_query_impl<int32_t>(pts_packed, ctr_packed, B, N, S, C, radius, K, out_idx, out_cnt, stream);
+    return ball_query_impl<int32_t>(pts_packed, ctr_packed, B, N, S, C, 1, &radius, &K, &out_idx,
+                                    out_cnt ? &out_cnt : nullptr, stream);
+}
+
+extern "C" int pn2_ball_query_multi_i32(const float *pts_packed, const float *ctr_packed, int64_t B,
+                                        int64_t N, int64_t S, int64_t C, int nr, const double *radii,
+                                        const int64_t *K, int32_t *const *out_idx, int32_t *const *out_cnt,
+                                        void *stream) {
+    return ball_query_impl<int32_t>(pts_packed, ctr_packed, B, N, S, C, nr, radii, K, out_idx, out_cnt,
+                                    stream);
 }
 
 // ------------------------------------------------------------------ square_distance

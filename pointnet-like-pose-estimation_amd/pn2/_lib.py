@@ -83,6 +83,7 @@ SIGNATURES = {
     "pn2_ball_query_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp]),
     "pn2_ball_query_cnt_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp, _vp]),
     "pn2_ball_query_i32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _dbl, _i64, _vp, _vp, _vp]),
+    "pn2_ball_query_multi_i32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _vp]),
     "pn2_square_distance_f32": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp]),
     "pn2_index_points_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp, _vp]),
     "pn2_group_f32": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64,

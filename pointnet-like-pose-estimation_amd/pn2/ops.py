@@ -221,6 +221,35 @@ def ball_query_direct(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: fl
     return (out, cnt) if with_count else out
 
 
+def ball_query_multi_direct(pts_packed: Tensor, ctr_packed: Tensor, C: int, radii, nsamples):
+    """ball_query_direct(..., with_count=True) for several radii of one centroid set (an MSG
+    layer's scales) in one launch (pn2_ball_query_multi_i32, up to 3 radii per launch): a list of
+    (group_idx [B,S,nsample] int32, counts [B,S] int32), the same as one call per radius."""
+    _dev(pts_packed, "pn2::ball_query")
+    B, N, cp = pts_packed.shape
+    S = ctr_packed.shape[1]
+    res = []
+    for i0 in range(0, len(radii), 3):
+        rs, ks = list(radii[i0:i0 + 3]), list(nsamples[i0:i0 + 3])
+        for k in ks:
+            if k > N:
+                raise IndexError("query_ball_point: sample_number %d > number of points %d" % (k, N))
+        outs = [torch.empty(B, S, k, dtype=torch.int32, device=pts_packed.device) for k in ks]
+        cnts = [torch.empty(B, S, dtype=torch.int32, device=pts_packed.device) for _ in ks]
+        nr = len(ks)
+        radii_c = (ctypes.c_double * nr)(*[float(r) for r in rs])
+        ks_c = (ctypes.c_int64 * nr)(*[int(k) for k in ks])
+        outs_c = (ctypes.c_void_p * nr)(*[t.data_ptr() for t in outs])
+        cnts_c = (ctypes.c_void_p * nr)(*[t.data_ptr() for t in cnts])
+        _run("pn2_ball_query_f32", _L.pn2_ball_query_multi_i32,
+             (pts_packed.data_ptr(), ctr_packed.data_ptr(), B, N, S, C, nr, radii_c, ks_c, outs_c, cnts_c,
+              _stream(pts_packed)), pts_packed.device,
+             nbytes=4.0 * cp * B * (N + S) + sum(4.0 * B * S * (k + 1) for k in ks),
+             flops=float(B) * S * N * (2 * C + 3))  # one distance per pair for all radii
+        res.extend(zip(outs, cnts))
+    return res
+
+
 def _ball_query_op(pts_packed: Tensor, ctr_packed: Tensor, C: int, radius: float, nsample: int) -> Tensor:
     return ball_query_direct(pts_packed, ctr_packed, C, radius, nsample)
 

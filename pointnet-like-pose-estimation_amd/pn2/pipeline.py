@@ -55,7 +55,7 @@ from . import geometry
 from . import ops
 from . import shard
 from . import tuning
-from .pointnet2_utils import PointNetSetAbstraction, PointNetSetAbstractionMsg
+from .pointnet2_utils import PointNetSetAbstraction, PointNetSetAbstractionMsg, msg_ball_queries
 
 _partitions = {}  # (device, geometry CUs) -> (geometry, compute, tail streams, raw handles)
 
@@ -278,11 +278,12 @@ class PipelinedForward:
                     newp, cpk, ppk = first[i]
                 else:
                     _, newp, cpk, ppk = ops.fps_direct(p, sa.point_number, starts[id(sa)])
-                if isinstance(sa, PointNetSetAbstractionMsg):
-                    rk = list(zip(sa.radius_list, sa.sample_number_list))
+                if not bq:
+                    idxs = []
+                elif isinstance(sa, PointNetSetAbstractionMsg):
+                    idxs = msg_ball_queries(ppk, cpk, C, sa.radius_list, sa.sample_number_list)
                 else:
-                    rk = [(sa.radius, sa.sample_number)]
-                idxs = [ops.ball_query_direct(ppk, cpk, C, r, kk, True) for r, kk in rk] if bq else []
+                    idxs = [ops.ball_query_direct(ppk, cpk, C, sa.radius, sa.sample_number, True)]
                 entries[id(sa)] = (p.data_ptr(), newp, cpk, ppk, idxs)
                 p = newp
         return entries

@@ -40,6 +40,7 @@ from . import geometry
 from . import ops
 from . import shard
 from . import train
+from . import tuning
 
 
 # ----------------------------------------------------------------------------- helpers
@@ -65,6 +66,15 @@ def _fps_ahead(module, new_points):
     job, (_, newp, cpk, ppk) = ops.fps_side_job(new_points, nxt.point_number, start)
     geometry.put_ahead(nxt, new_points, newp, cpk, ppk)
     return job
+
+
+def msg_ball_queries(ppk, cpk, C, radii, nsamples):
+    """The ball queries of an MSG layer's scales (pointnet2_utils.py:197-203): one launch over
+    all radii (ops.ball_query_multi_direct; host tuning bq_multi = 0: one call per radius), the
+    same (int32 lists, counts) per radius either way."""
+    if tuning.get("bq_multi") and len(radii) > 1:
+        return ops.ball_query_multi_direct(ppk, cpk, C, radii, nsamples)
+    return [ops.ball_query_direct(ppk, cpk, C, r, k, True) for r, k in zip(radii, nsamples)]
 
 
 def _channels_last(feature):
@@ -338,13 +348,11 @@ class PointNetSetAbstractionMsg(nn.Module):
         if pre is not None:
             new_points, cpk, ppk, idxs = pre
             if not idxs:
-                idxs = [ops.ball_query_direct(ppk, cpk, C, r, k, True)
-                        for r, k in zip(self.radius_list, self.sample_number_list)]
+                idxs = msg_ball_queries(ppk, cpk, C, self.radius_list, self.sample_number_list)
         else:
             with geometry.Span(dev, [pts]) as span:  # overlaps the previous layer's MLP
                 _, new_points, cpk, ppk = ops.fps_direct(pts, S, _draw_start(B, N, dev))
-                idxs = [ops.ball_query_direct(ppk, cpk, C, r, k, True)
-                        for r, k in zip(self.radius_list, self.sample_number_list)]
+                idxs = msg_ball_queries(ppk, cpk, C, self.radius_list, self.sample_number_list)
             span.finish([new_points], [new_points] + [t for ic in idxs for t in ic])
         out = torch.empty(B * S, total, device=dev, dtype=torch.float32)
         prec = _precision(self)

@@ -26,6 +26,8 @@ Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_s
                      0: only the FPS, each batch's forward (compute stream) queries
     pipe_fuse        1: GraphedPipeline runs one forward (sa + head graphs) per geometry group,
                      its batches side by side; 0: one forward per batch
+    bq_multi         1: an MSG layer's ball queries in one launch over its radii
+                     (pn2_ball_query_multi_i32); 0: one launch per radius
     pipe_profile     1: the pipelines (pn2.pipeline) capture and run their kernels under
                      PIPELINE_PROFILE -- the launch choices measured best beside each other's
                      kernels, where the kernel defaults are the ones measured best alone (the
@@ -52,6 +54,7 @@ HOST_DEFAULTS = {
     "tail_streams": 1,
     "geometry_bq": 1,
     "pipe_fuse": 1,
+    "bq_multi": 1,
 }
 
 

@@ -289,3 +289,29 @@ def test_fps_host_start_out_of_range_raises():
     pd = torch.rand(2, 64, 3, device=DEV)
     with pytest.raises(RuntimeError, match="start"):
         ops.fps_direct(pd, 8, torch.tensor([3, 64]))
+
+
+# pn2_ball_query_multi_i32: an MSG layer's radii in one launch == one pn2_ball_query_i32 per
+# radius, bit for bit (lists and counts), on LDS row buffers and direct row writes, C = 3 / 10,
+# partial 32-point words, early exit (dense radius) and a radius with no neighbours
+@pytest.mark.parametrize("C,N,S,radii,ks,rowbuf", [
+    (3, 4096, 512, [0.1, 0.2, 0.4], [16, 32, 128], 96),   # MSG sa1
+    (3, 512, 128, [0.2, 0.4, 0.8], [32, 64, 128], 96),    # MSG sa2
+    (3, 1000, 100, [0.05, 0.3], [8, 40], 96),             # partial words, two radii
+    (10, 2048, 256, [0.1, 0.2, 0.4], [16, 32, 64], 96),   # pose channels
+    (3, 4096, 512, [0.1, 0.2, 0.4], [16, 32, 128], 0),    # rows straight to HBM
+    (3, 700, 64, [1e-6, 0.3, 2.5], [4, 16, 700], 96),     # no neighbours / whole cloud
+])
+def test_ball_query_multi_matches_single(C, N, S, radii, ks, rowbuf):
+    from pn2 import ops, tuning
+    B = 3
+    pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 41).to(DEV)
+    ctr = pts[:, :S].contiguous()
+    ppk, cpk = ops.pack_points_direct(pts), ops.pack_points_direct(ctr)
+    with tuning.override(bq_rowbuf_kb=rowbuf):
+        multi = ops.ball_query_multi_direct(ppk, cpk, C, radii, ks)
+        single = [ops.ball_query_direct(ppk, cpk, C, r, k, True) for r, k in zip(radii, ks)]
+    from pn2 import _lib
+    _lib.device_errors(DEV)  # (the 1e-6 radius may leave centroids without neighbours: flagged)
+    for (a, ca), (b, cb) in zip(multi, single):
+        assert torch.equal(a, b) and torch.equal(ca, cb)

@@ -2,7 +2,8 @@
 tools/debug/build_dense_stamps.sh): PN2_DEBUG_LIB=.../pn2/var/dstamps.so python tools/debug/dense_stamps.py
 Runs one eager SSG B=32 N=1024 forward after warm-up; the last dense launch of it is sa3's
 512 -> 1024 layer (group_all, pooled over the 128 points of a cloud); CONFIG=pose: translation_ssg's
-sa2 512 -> 1024 layer at B=64 (GRID=1024 wide tiles, NST=8).  Prints the spread of
+sa2 512 -> 1024 layer at B=64 (GRID=1024 wide tiles, NST=8); B=<n> the SSG batch (B=128: the
+pipeline's four-batch group), DENSE_LDS=0 the register-staged kernel the pipeline runs.  Prints the spread of
 workgroup start times, percentiles of the prologue (entry -> stage 0 landed), of each stage
 (barrier to barrier), of the epilogue, and of the workgroup lifetime."""
 import ctypes
@@ -34,8 +35,10 @@ if pose:
     x = cases.cloud("onehot10", 64, 2048, 90).permute(0, 2, 1).contiguous().to(DEV)
     args = (x, torch.zeros(64, 3, device=DEV))
 else:
-    args = (cases.cloud("uniform3", 32, 1024, 90).permute(0, 2, 1).contiguous().to(DEV),)
-with torch.no_grad():
+    args = (cases.cloud("uniform3", int(os.environ.get("B", "32")), 1024, 90).permute(0, 2, 1).contiguous().to(DEV),)
+from pn2 import tuning  # noqa: E402
+ov = {"dense_lds": int(os.environ["DENSE_LDS"])} if "DENSE_LDS" in os.environ else {}
+with torch.no_grad(), tuning.override(**ov):
     for _ in range(5):
         model(*args)
     torch.cuda.synchronize()
