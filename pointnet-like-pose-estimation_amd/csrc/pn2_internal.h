@@ -37,6 +37,7 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
     X(mlp_f32, 0)          /* 1: fp32 MFMA kernels instead of the split-bf16 ones          */ \
     X(chain_f16, 1)        /* 1: fp32-accurate chains as split fp16 (3 MFMAs per product)   */ \
     X(dense_frag, 1)       /* 1: dense hidden rows in MFMA-fragment order (register kernel) */ \
+    X(dense_pair, 1)       /* 1: group_all's first two dense layers as one launch          */ \
     X(dense_f16, 1)        /* split fp16 dense layers: 1 after the first, 2 also the first  */ \
                            /* where eligible; 0: split bf16 (6)                             */ \
     X(chain_prepass, 1)    /* 0: no layer-0 pre-pass (wide first layers of a chain)        */ \

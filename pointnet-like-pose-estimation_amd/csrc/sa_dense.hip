@@ -33,10 +33,16 @@ namespace pn2 {
 #ifdef PN2_DENSE_STAMPS
 constexpr int kDStampWG = 4096, kDStamps = 18;
 __device__ unsigned long long g_dense_stamps[kDStampWG * kDStamps];
+// launches stamped: every one (-1, the last one wins) or those with mode * 1000 + tiles == sel
+__device__ int g_dense_sel = -1;
+extern "C" int pn2_debug_dense_select(int sel) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_dense_sel), &sel, sizeof(int)) == hipSuccess ? 0 : -1;
+}
+#define PN2_DSEL (g_dense_sel < 0 || g_dense_sel == A.mode * 1000 + A.tiles)
 #define PN2_DSTAMP(i)                                                                           \
     do {                                                                                        \
         const unsigned b_ = blockIdx.x + blockIdx.y * gridDim.x;                                \
-        if (threadIdx.x == 0 && b_ < kDStampWG)                                                 \
+        if (threadIdx.x == 0 && b_ < kDStampWG && PN2_DSEL)                                     \
             g_dense_stamps[b_ * kDStamps + (i)] = __builtin_amdgcn_s_memrealtime();             \
     } while (0)
 extern "C" int pn2_debug_dense_stamps(unsigned long long *dst, int64_t n) {
@@ -46,7 +52,7 @@ extern "C" int pn2_debug_dense_stamps(unsigned long long *dst, int64_t n) {
 #define PN2_DCLOCK(i)                                                                           \
     do {                                                                                        \
         const unsigned b_ = blockIdx.x + blockIdx.y * gridDim.x;                                \
-        if (threadIdx.x == 0 && b_ < kDStampWG)                                                 \
+        if (threadIdx.x == 0 && b_ < kDStampWG && PN2_DSEL)                                     \
             g_dense_stamps[b_ * kDStamps + (i)] = __builtin_amdgcn_s_memtime();                 \
     } while (0)
 #else
@@ -939,6 +945,261 @@ static int launch_dense_lds_tile(int tile, const DenseSplitArgs &A, int np, hipS
 #undef PN2_LDS_NP
 }
 
+// ------------------------------------------------------------------ fused group_all layer pair
+// The first two layers of a group_all MLP (sa3: [xyz | 256 features] -> 256 -> 512) in one
+// launch, the 256-wide intermediate never leaving the CU.  Taken one per launch, those two
+// layers are each ~6 us of fixed cost (the first DMA's latency, the store drain at the end)
+// around 5-7 us of stages (tools/debug/dense_stamps.py SEL=1008 / 16).
+// Workgroup = one 32-row block x one of `cs` column slices of the second layer, 8 waves:
+//   1. the block's layer-0 A operand split once into LDS planes [kb][NP0][64 lanes][16 B]
+//      (wave w splits k-blocks w, w + 8, ...);
+//   2. wave w: layer-0 column tile w over every k-block, its weight fragments streamed straight
+//      into registers RD k-blocks ahead (nothing else to share: each wave has its own tile);
+//   3. BN + ReLU in registers; the block's max |value| (the maxima the unfused layer 0 would
+//      leave for layer 1) through LDS; every value split (elementwise, scaled for NP1 = 2) and
+//      written into layer 1's A planes, which replace layer 0's;
+//   4. wave w: layer-1 column tile (slice * 8 + w), weights streamed the same way (its first
+//      k-blocks already requested behind step 2), epilogue as dense_lds_kernel's (rows or
+//      fragment order, out_max for layer 2).
+// Layer 0 is computed once per slice (cs = 2 for 512 outputs: 256 workgroups at SSG's 4096
+// rows).  Products, accumulation order, scales and epilogues are the unfused layers': the same
+// bits (tests/test_gpu_mlp.py).
+template <int NP>
+__device__ __forceinline__ Split load_wfrag(const bf16x8 *wq, int64_t plane) {
+    Split w;
+    w.h = wq[0];
+    w.m = NP >= 2 ? wq[plane] : w.h;
+    w.l = NP == 3 ? wq[2 * plane] : w.h;
+    return w;
+}
+
+constexpr int kPairWaves = 8, kPairRD = 8;
+
+template <int NP0, int NP1, int KB0>
+__global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const DenseSplitArgs A0, const DenseSplitArgs A1,
+                                                                     int cs) {
+    // k-block counts are compile-time (layer 1's input is layer 0's 8 tiles): fully unrolled,
+    // branch-free weight streams whose vmcnt waits the compiler counts exactly
+    constexpr int NW = kPairWaves, RD = kPairRD, KB1 = 2 * kPairWaves;
+    extern __shared__ __attribute__((aligned(16))) char psm[];
+    unsigned *smax = reinterpret_cast<unsigned *>(psm);  // [NW] layer-0 tile maxima
+    char *planes = psm + 64;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int r = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const unsigned lid = xcd_contiguous(blockIdx.x, gridDim.x);
+    const int rb = (int)(lid / (unsigned)cs), slice = (int)(lid % (unsigned)cs);
+    const int row0 = 32 * rb;
+    const int M = A0.M;
+    if (A1.zero) {  // side job: the next layer's pool
+        const int64_t tot = A1.zrows * A1.zcols, nwg = gridDim.x;
+        const int64_t per = (tot + nwg - 1) / nwg, e0 = (int64_t)blockIdx.x * per;
+        const int64_t e1 = e0 + per < tot ? e0 + per : tot;
+        for (int64_t e = e0 + tid; e < e1; e += 64 * NW) {
+            const int64_t g = e / A1.zcols;
+            A1.zero[g * A1.zstride + (e - g * A1.zcols)] = 0.f;
+        }
+    }
+    // layer-0 weights of this wave's tile: the first RD k-blocks requested now
+    constexpr int kb0n = KB0, kb1n = KB1;
+    const int64_t plane0 = (int64_t)A0.tiles * kb0n * 64, plane1 = (int64_t)A1.tiles * kb1n * 64;
+    const bf16x8 *w0 = A0.w + (int64_t)wave * kb0n * 64 + lane;
+    const int t1 = slice * NW + wave;
+    const bf16x8 *w1 = A1.w + (int64_t)t1 * kb1n * 64 + lane;
+    // both epilogues' BN scale / shift, loaded first (a load behind the weight stream would wait
+    // for all of it); layer 1's scale still lacks the activation down-scale (dense_alpha's last
+    // factor)
+    const int col0 = 32 * wave + r, col1 = 32 * t1 + r;
+    const float al0 = dense_alpha<NP0>(A0, col0, 1.f), be0 = A0.raw ? 0.f : A0.beta[col0];
+    const float pa1 = NP1 == 2 ? (A1.raw ? 1.f : A1.alpha[col1]) * A1.wscale[col1] : dense_alpha<NP1>(A1, col1, 1.f);
+    const float be1 = A1.raw ? 0.f : A1.beta[col1];
+    Split wb[RD];
+#pragma unroll
+    for (int i = 0; i < RD; ++i)
+        if (i < kb0n) wb[i] = load_wfrag<NP0>(w0 + i * 64, plane0);
+
+    // ---- 1. layer-0 A planes
+    {
+        const int R = min(row0 + r, M - 1);  // rows past M: any valid row, never stored
+        const int b = R / A0.N, n = R - b * A0.N;
+        for (int kb = wave; kb < kb0n; kb += NW) {
+            float x[8];
+            if (kb == 0) {  // raw xyz (sample_and_group_all does not centre)
+                const float *prow = A0.pts + (int64_t)b * A0.pb + (int64_t)n * A0.pn;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int ch = (j & 3) + 8 * (j >> 2) + 4 * h;
+                    x[j] = ch < A0.C ? prow[(int64_t)ch * A0.pc] : 0.f;
+                }
+            } else {
+                const float *f = A0.feat + (int64_t)b * A0.fb + (int64_t)n * A0.fn + 16 * (kb - 1) + 4 * h;
+                const cfloatx4 q0 = *reinterpret_cast<const cfloatx4 *>(f);
+                const cfloatx4 q1 = *reinterpret_cast<const cfloatx4 *>(f + 8);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[i] = q0[i], x[4 + i] = q1[i];
+            }
+            const Split s = splitN<NP0>(x);
+            bf16x8 *dst = reinterpret_cast<bf16x8 *>(planes + kb * NP0 * 1024) + lane;
+            dst[0] = s.h;
+            if (NP0 >= 2) dst[64] = s.m;
+            if (NP0 == 3) dst[128] = s.l;
+        }
+    }
+    // barriers without __syncthreads' vmcnt(0): the weight prefetches stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stage_barrier();
+
+    // ---- 2. layer 0, tile `wave`
+    cfloatx16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    // per k-block, in this order (sched_barrier: the scheduler would sink the weight requests
+    // under the MFMAs and leave one or two in flight): the next k-block's A planes from LDS,
+    // this k-block's MFMAs, the request RD k-blocks ahead into the register just consumed
+    Split xn = ring_readN<NP0>(planes, lane);
+#pragma unroll
+    for (int kb = 0; kb < kb0n; ++kb) {
+        const Split xs = xn;
+        if (kb + 1 < kb0n) xn = ring_readN<NP0>(planes + (kb + 1) * NP0 * 1024, lane);
+        acc = mma_wb<NP0>(xs, wb[kb % RD], acc);
+        if (kb + RD < kb0n) wb[kb % RD] = load_wfrag<NP0>(w0 + (int64_t)(kb + RD) * 64, plane0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // layer-1 weights: the first RD k-blocks requested behind layer 0's MFMAs
+    Split wc[RD];
+#pragma unroll
+    for (int i = 0; i < RD; ++i) wc[i] = load_wfrag<NP1>(w1 + i * 64, plane1);
+
+    // ---- 3. layer-0 epilogue -> layer-1 A planes
+    float v[16];
+    unsigned tmax = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int row = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const float y = __builtin_fmaf(acc[q], al0, be0);
+        v[q] = A0.raw ? acc[q] * al0 : (A0.norelu ? y : chain_relu(y));
+        if (row < M) tmax = max(tmax, __float_as_uint(v[q]) & 0x7FFFFFFFu);
+    }
+    tmax = wave_max_u32(tmax);
+    if (lane == 0) smax[wave] = tmax;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stage_barrier();  // the maxima are in; every wave's layer-0 plane reads returned
+    ActScale asc{1.f, 1.f};
+    if constexpr (NP1 == 2) {
+        unsigned m = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) m = max(m, smax[i]);
+        asc = act_scale(__uint_as_float(m));
+    }
+    {
+        // element (row, col) of the block -> layer-1 k-block col / 16, lane (row & 31) + 32 h',
+        // element j of that lane's 8 (channel c = col % 16 = (j & 3) + 8 (j >> 2) + 4 h')
+        const int kb = col0 >> 4, c = col0 & 15;
+        const int hh = (c >> 2) & 1, j = (c & 3) + 4 * (c >> 3);
+        char *base = planes + kb * NP1 * 1024 + 32 * hh * 16 + j * 2;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int rr = (q & 3) + 8 * (q >> 2) + 4 * h;
+            char *p = base + rr * 16;
+            if constexpr (NP1 == 2) {
+                const float y = v[q] * asc.up;
+                const _Float16 a = (_Float16)y;
+                const _Float16 b2 = (_Float16)(y - (float)a);
+                *reinterpret_cast<_Float16 *>(p) = a;
+                *reinterpret_cast<_Float16 *>(p + 1024) = b2;
+            } else if constexpr (NP1 == 3) {
+                const __bf16 a = (__bf16)v[q];
+                const float r1 = v[q] - (float)a;
+                const __bf16 b2 = (__bf16)r1;
+                const float r2 = r1 - (float)b2;
+                *reinterpret_cast<__bf16 *>(p) = a;
+                *reinterpret_cast<__bf16 *>(p + 1024) = b2;
+                *reinterpret_cast<__bf16 *>(p + 2048) = (__bf16)r2;
+            } else {
+                *reinterpret_cast<__bf16 *>(p) = (__bf16)v[q];
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stage_barrier();
+
+    // ---- 4. layer 1, tile t1
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    Split yn = ring_readN<NP1>(planes, lane);
+#pragma unroll
+    for (int kb = 0; kb < kb1n; ++kb) {
+        const Split xs = yn;
+        if (kb + 1 < kb1n) yn = ring_readN<NP1>(planes + (kb + 1) * NP1 * 1024, lane);
+        acc = mma_wb<NP1>(xs, wc[kb % RD], acc);
+        if (kb + RD < kb1n) wc[kb % RD] = load_wfrag<NP1>(w1 + (int64_t)(kb + RD) * 64, plane1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const float al1 = NP1 == 2 ? pa1 * asc.down : pa1;
+    unsigned omax = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int row = row0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (row < M) {
+            const float y = __builtin_fmaf(acc[q], al1, be1);
+            const float o = A1.raw ? acc[q] * al1 : (A1.norelu ? y : chain_relu(y));
+            A1.out[A1.frag_out ? frag_off(row, col1, 2 * A1.tiles) : (int64_t)row * A1.ostride + col1] = o;
+            omax = max(omax, __float_as_uint(o) & 0x7FFFFFFFu);
+        }
+    }
+    if (A1.out_max) {
+        const unsigned m = wave_max_u32(omax);
+        if (lane == 0 && row0 < M) A1.out_max[(int64_t)rb * A1.tiles + t1] = m;
+    }
+}
+
+// The pair's LDS: the maxima + the larger layer's A planes
+static size_t dense_pair_lds(const DenseSplitArgs &A0, const DenseSplitArgs &A1, int np0, int np1) {
+    return 64 + (size_t)std::max(A0.kb * np0, A1.kb * np1) * 1024;
+}
+
+// Whether layers A0 (group_all, first) and A1 (its consumer) run as one dense_pair_kernel
+// launch: layer 0 = 8 column tiles (256 outputs: one per wave), layer 1 reads all of them and
+// has a multiple of 8 tiles, neither pools, rows of 16-byte feature runs.
+static bool dense_pair_ok(const DenseSplitArgs &A0, const DenseSplitArgs &A1, int np0, int np1) {
+    if (!tuning().dense_pair || A0.mode != 1 || A1.mode != 0 || A0.pool || A1.pool) return false;
+    if (A0.tiles != kPairWaves || A1.tiles % kPairWaves != 0 || A1.cin != 32 * A0.tiles || A1.kb != 2 * A0.tiles)
+        return false;
+    if (!A0.vec || !A0.feat || A0.D <= 0 || A0.D % 16 != 0 || A0.kb != 1 + A0.D / 16 || A0.C > 16) return false;
+    if (A0.fn % 4 || A0.fb % 4 || ((uintptr_t)A0.feat & 15)) return false;
+    if (np0 != 3 || (np1 != 2 && np1 != 3)) return false;
+    if (A0.kb != 17 && A0.kb != 41) return false;  // the instantiated k-block counts (D = 256, 640)
+    if (np1 == 2 && !A1.wscale) return false;
+    if (A1.frag_in) return false;
+    return dense_pair_lds(A0, A1, np0, np1) <= 160 * 1024;
+}
+
+template <int NP0, int NP1, int KB0>
+static void launch_pair(const DenseSplitArgs &A0, const DenseSplitArgs &A1, int cs, dim3 grid, dim3 block, size_t lds,
+                        hipStream_t st) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&dense_pair_kernel<NP0, NP1, KB0>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)attr;
+    hipLaunchKernelGGL((dense_pair_kernel<NP0, NP1, KB0>), grid, block, lds, st, A0, A1, cs);
+}
+
+static int launch_dense_pair(const DenseSplitArgs &A0, const DenseSplitArgs &A1, int np1, hipStream_t st) {
+    const int cs = A1.tiles / kPairWaves;
+    const int64_t nrb = (A0.M + 31) / 32;
+    const size_t lds = dense_pair_lds(A0, A1, 3, np1);
+    const dim3 grid((unsigned)(nrb * cs)), block(64 * kPairWaves);
+    if (np1 == 2) {
+        if (A0.kb == 17) launch_pair<3, 2, 17>(A0, A1, cs, grid, block, lds, st);
+        else launch_pair<3, 2, 41>(A0, A1, cs, grid, block, lds, st);
+    } else {
+        if (A0.kb == 17) launch_pair<3, 3, 17>(A0, A1, cs, grid, block, lds, st);
+        else launch_pair<3, 3, 41>(A0, A1, cs, grid, block, lds, st);
+    }
+    PN2_LAUNCH_CHECK("dense_pair_kernel");
+    return PN2_OK;
+}
+
 // Large split (fp32-accurate) layers take 256 x 128 tiles (see dense_split_layer); the rows a
 // launch's workgroup covers decide which pools fit in LDS.  bf16 layers keep the 128-row tiles:
 // with one MFMA per product instead of six the big tile's one workgroup per CU (8 waves, 221
@@ -1162,15 +1423,30 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
         last.zcols = s.zero_count;
         last.zstride = s.zero_count;
     }
-    int64_t flops[4] = {0, 0, 0, 0};
-    for (int l = 0; l < nlayers; ++l) {
-        flops[layer_np(l)] += layers[l].cin * layers[l].cout;
+    auto args_of = [&](int l) {
         DenseSplitArgs A = l == nlayers - 1 ? last : make_f(l);
         if (fold_zero && l == nlayers - 2) {
             A.zero = last.out;
             A.zrows = last.M / last.K;
             A.zcols = 32 * (int64_t)last.tiles;
             A.zstride = last.ostride;
+        }
+        return A;
+    };
+    int64_t flops[4] = {0, 0, 0, 0};
+    for (int l = 0; l < nlayers; ++l) {
+        flops[layer_np(l)] += layers[l].cin * layers[l].cout;
+        DenseSplitArgs A = args_of(l);
+        if (l == 0 && nlayers > 1) {  // group_all's first two layers as one launch
+            DenseSplitArgs B = args_of(1);
+            B.frag_in = 0;  // its input never leaves the CU
+            if (dense_pair_ok(A, B, layer_np(0), layer_np(1))) {
+                const int rc = launch_dense_pair(A, B, layer_np(1), st);
+                if (rc != PN2_OK) return rc;
+                flops[layer_np(1)] += layers[1].cin * layers[1].cout;
+                l = 1;
+                continue;
+            }
         }
         const int rc = dense_split_layer(A, layer_np(l), st, fold_zero && l == nlayers - 1);
         if (rc != PN2_OK) return rc;

@@ -298,6 +298,43 @@ def test_dense_frag_rows_bit_identical(case, prec):
     np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
 
 
+# group_all MLPs whose first two layers run as one dense_pair_kernel launch (256 outputs, then a
+# multiple of 256): SSG / POSE sa3 (D = 256), MSG sa3 (D = 640), a partial last 32-row block with
+# clouds that do not fill whole blocks (N = 40: split bf16 throughout)
+DENSE_PAIR = [
+    (3, 256, 128, [256, 512, 1024], 32),
+    (3, 640, 128, [256, 512, 1024], 6),
+    (10, 256, 64, [256, 256, 512], 3),
+    (3, 256, 40, [256, 512, 1024], 3),
+]
+
+
+@pytest.mark.parametrize("f16", [1, 0])
+@pytest.mark.parametrize("lds", [1, 0])
+@pytest.mark.parametrize("case", range(len(DENSE_PAIR)))
+def test_dense_pair_bit_identical(case, lds, f16):
+    """The fused first two group_all layers (tuning dense_pair = 1) vs the layers one launch each:
+    the same products, accumulation order, scales and epilogues -- the same bits, with the third
+    layer on either dense kernel (rows or fragment order) and layer 1 split fp16 or bf16."""
+    import pn2
+    from pn2 import tuning
+    C, D, N, mlp, B = DENSE_PAIR[case]
+    pts = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 950 + case)
+    feat = torch.randn(B, N, D, generator=torch.Generator().manual_seed(960 + case)) * (1 + 3 * case)
+    torch.manual_seed(case)
+    sa = pn2.PointNetSetAbstraction(None, None, None, C + D, mlp, True)
+    cases.randomize_bn(sa, case)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous().to(DEV)
+    f = feat.permute(0, 2, 1).contiguous().to(DEV)
+    outs = []
+    for pair in (1, 0):
+        with torch.no_grad(), tuning.override(dense_pair=pair, dense_lds=lds, dense_f16=f16):
+            outs.append(sa(x, f)[1].cpu().numpy())
+    assert np.isfinite(outs[0]).all()
+    np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
 def test_dense_lds_rows_source_v1():
     """PointNet-v1 encoder MLPs (rows source, unpooled and max over N = 1024 points, the last
     layer signed / without ReLU): LDS-staged == register-staged bits."""

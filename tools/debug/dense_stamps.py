@@ -1,7 +1,7 @@
 """Per-workgroup timeline of the dense layer kernel (diagnostic build,
 tools/debug/build_dense_stamps.sh): PN2_DEBUG_LIB=.../pn2/var/dstamps.so python tools/debug/dense_stamps.py
 Runs one eager SSG B=32 N=1024 forward after warm-up; the last dense launch of it is sa3's
-512 -> 1024 layer (group_all, pooled over the 128 points of a cloud); CONFIG=pose: translation_ssg's
+512 -> 1024 layer (group_all, pooled over the 128 points of a cloud); SEL selects another launch (below); CONFIG=pose: translation_ssg's
 sa2 512 -> 1024 layer at B=64 (GRID=1024 wide tiles, NST=8); B=<n> the SSG batch (B=128: the
 pipeline's four-batch group), DENSE_LDS=0 the register-staged kernel the pipeline runs.  Prints the spread of
 workgroup start times, percentiles of the prologue (entry -> stage 0 landed), of each stage
@@ -25,6 +25,8 @@ from pn2 import heads as H  # noqa: E402
 DEV = torch.device("cuda", 0)
 fn = _lib.load().pn2_debug_dense_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+# SEL=<mode * 1000 + output tiles>: stamp only those launches (SEL=1008: sa3's first layer)
+assert _lib.load().pn2_debug_dense_select(int(os.environ.get("SEL", "-1"))) == 0
 NW, NS = 4096, 18
 torch.manual_seed(8)
 pose = os.environ.get("CONFIG", "ssg") == "pose"  # translation_ssg B=64 N=2048: group_all over 32768 rows
