@@ -973,7 +973,10 @@ __device__ __forceinline__ Split load_wfrag(const bf16x8 *wq, int64_t plane) {
     return w;
 }
 
-constexpr int kPairWaves = 8, kPairRD = 8;
+#ifndef PN2_PAIR_RD
+#define PN2_PAIR_RD 4
+#endif
+constexpr int kPairWaves = 8, kPairRD = PN2_PAIR_RD;  // k-blocks of weights in flight per wave
 
 template <int NP0, int NP1, int KB0>
 __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const DenseSplitArgs A0, const DenseSplitArgs A1,
@@ -981,6 +984,9 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
     // k-block counts are compile-time (layer 1's input is layer 0's 8 tiles): fully unrolled,
     // branch-free weight streams whose vmcnt waits the compiler counts exactly
     constexpr int NW = kPairWaves, RD = kPairRD, KB1 = 2 * kPairWaves;
+    const DenseSplitArgs &A = A0;  // the stamps' launch selection (diagnostic builds)
+    (void)A;
+    PN2_DSTAMP(0);
     extern __shared__ __attribute__((aligned(16))) char psm[];
     unsigned *smax = reinterpret_cast<unsigned *>(psm);  // [NW] layer-0 tile maxima
     char *planes = psm + 64;
@@ -1001,7 +1007,6 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
             A1.zero[g * A1.zstride + (e - g * A1.zcols)] = 0.f;
         }
     }
-    // layer-0 weights of this wave's tile: the first RD k-blocks requested now
     constexpr int kb0n = KB0, kb1n = KB1;
     const int64_t plane0 = (int64_t)A0.tiles * kb0n * 64, plane1 = (int64_t)A1.tiles * kb1n * 64;
     const bf16x8 *w0 = A0.w + (int64_t)wave * kb0n * 64 + lane;
@@ -1014,41 +1019,52 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
     const float al0 = dense_alpha<NP0>(A0, col0, 1.f), be0 = A0.raw ? 0.f : A0.beta[col0];
     const float pa1 = NP1 == 2 ? (A1.raw ? 1.f : A1.alpha[col1]) * A1.wscale[col1] : dense_alpha<NP1>(A1, col1, 1.f);
     const float be1 = A1.raw ? 0.f : A1.beta[col1];
-    Split wb[RD];
-#pragma unroll
-    for (int i = 0; i < RD; ++i)
-        if (i < kb0n) wb[i] = load_wfrag<NP0>(w0 + i * 64, plane0);
 
-    // ---- 1. layer-0 A planes
+    // ---- 1. layer-0 A planes: this wave's k-blocks w, w + 8, ... all requested at once, then
+    // the layer-0 weights' first RD k-blocks behind them, then the splits
+    constexpr int PER = (KB0 + NW - 1) / NW;
+    float xa[PER][8];
     {
         const int R = min(row0 + r, M - 1);  // rows past M: any valid row, never stored
         const int b = R / A0.N, n = R - b * A0.N;
-        for (int kb = wave; kb < kb0n; kb += NW) {
-            float x[8];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int kb = wave + NW * i;
             if (kb == 0) {  // raw xyz (sample_and_group_all does not centre)
                 const float *prow = A0.pts + (int64_t)b * A0.pb + (int64_t)n * A0.pn;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int ch = (j & 3) + 8 * (j >> 2) + 4 * h;
-                    x[j] = ch < A0.C ? prow[(int64_t)ch * A0.pc] : 0.f;
+                    xa[i][j] = ch < A0.C ? prow[(int64_t)ch * A0.pc] : 0.f;
                 }
-            } else {
+            } else if (kb < kb0n) {
                 const float *f = A0.feat + (int64_t)b * A0.fb + (int64_t)n * A0.fn + 16 * (kb - 1) + 4 * h;
                 const cfloatx4 q0 = *reinterpret_cast<const cfloatx4 *>(f);
                 const cfloatx4 q1 = *reinterpret_cast<const cfloatx4 *>(f + 8);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) x[i] = q0[i], x[4 + i] = q1[i];
+                for (int j = 0; j < 4; ++j) xa[i][j] = q0[j], xa[i][4 + j] = q1[j];
             }
-            const Split s = splitN<NP0>(x);
+        }
+    }
+    Split wb[RD];
+#pragma unroll
+    for (int i = 0; i < RD; ++i)
+        if (i < kb0n) wb[i] = load_wfrag<NP0>(w0 + i * 64, plane0);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int kb = wave + NW * i;
+        if (kb < kb0n) {
+            const Split sp = splitN<NP0>(xa[i]);
             bf16x8 *dst = reinterpret_cast<bf16x8 *>(planes + kb * NP0 * 1024) + lane;
-            dst[0] = s.h;
-            if (NP0 >= 2) dst[64] = s.m;
-            if (NP0 == 3) dst[128] = s.l;
+            dst[0] = sp.h;
+            if (NP0 >= 2) dst[64] = sp.m;
+            if (NP0 == 3) dst[128] = sp.l;
         }
     }
     // barriers without __syncthreads' vmcnt(0): the weight prefetches stay in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     stage_barrier();
+    PN2_DSTAMP(1);
 
     // ---- 2. layer 0, tile `wave`
     cfloatx16 acc;
@@ -1066,6 +1082,7 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
         if (kb + RD < kb0n) wb[kb % RD] = load_wfrag<NP0>(w0 + (int64_t)(kb + RD) * 64, plane0);
         __builtin_amdgcn_sched_barrier(0);
     }
+    PN2_DSTAMP(2);
     // layer-1 weights: the first RD k-blocks requested behind layer 0's MFMAs
     Split wc[RD];
 #pragma unroll
@@ -1085,6 +1102,7 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
     if (lane == 0) smax[wave] = tmax;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     stage_barrier();  // the maxima are in; every wave's layer-0 plane reads returned
+    PN2_DSTAMP(3);
     ActScale asc{1.f, 1.f};
     if constexpr (NP1 == 2) {
         unsigned m = 0;
@@ -1123,6 +1141,7 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     stage_barrier();
+    PN2_DSTAMP(4);
 
     // ---- 4. layer 1, tile t1
 #pragma unroll
@@ -1136,6 +1155,8 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
         if (kb + RD < kb1n) wc[kb % RD] = load_wfrag<NP1>(w1 + (int64_t)(kb + RD) * 64, plane1);
         __builtin_amdgcn_sched_barrier(0);
     }
+    PN2_DSTAMP(5);
+    PN2_DSTAMP(14);
     const float al1 = NP1 == 2 ? pa1 * asc.down : pa1;
     unsigned omax = 0;
 #pragma unroll
@@ -1152,6 +1173,7 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
         const unsigned m = wave_max_u32(omax);
         if (lane == 0 && row0 < M) A1.out_max[(int64_t)rb * A1.tiles + t1] = m;
     }
+    PN2_DSTAMP(15);
 }
 
 // The pair's LDS: the maxima + the larger layer's A planes

@@ -5,7 +5,7 @@ The product path reads one environment variable, once, at import:
     PN2_TUNING="key=value,key=value,..."
 
 Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_set``:
-``mlp_f32``, ``chain_prepass``, ``compact``, ``compact_pool``, ``compact_stages``,
+``mlp_f32``, ``chain_prepass``, ``dense_pair``, ``compact``, ``compact_pool``, ``compact_stages``,
 ``bq_waves``, ``bq_rowbuf_kb``, ``fps_threads``, ``fps_ppt``, ``fps_mid``, ``dense_maxntc``,
 ``dense_minwg``, ``dense_wide_minwg``, ``dense_lds``, ``dense_lds_stages``, ``dense_lds_xcd2d``,
 ``dense_lds_tile``; csrc/pn2_internal.h documents each) and these host-side ones:
@@ -74,9 +74,12 @@ _host.update({k: v for k, v in _ENV.items() if k in HOST_DEFAULTS})
 
 
 # Kernel keys the pipelines set while they capture / run: the FPS block of 4
-# waves x 4 points, the register-staged dense kernel and 8-wave ball-query workgroups (for
-# clouds below 2048 points) -- each faster alone in the other form, slower beside the chains.
-PIPELINE_PROFILE = {"fps_mid": 256, "dense_lds": 0, "bq_waves": 0}
+# waves x 4 points, the register-staged dense kernel, 8-wave ball-query workgroups (for
+# clouds below 2048 points) and group_all's first two layers one launch each (the fused pair
+# streams both layers' weights per 32-row block: at a fused group's 16384 rows that L2 -> CU
+# stream costs more than the launch it saves, SSG K=100 192.2k with it vs 195.3k) -- each
+# faster alone in the other form, slower beside the chains.
+PIPELINE_PROFILE = {"fps_mid": 256, "dense_lds": 0, "bq_waves": 0, "dense_pair": 0}
 
 
 @contextlib.contextmanager

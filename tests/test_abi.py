@@ -193,7 +193,7 @@ def test_pipeline_profile_keeps_explicit_keys():
     with tuning.pipeline_profile():
         assert tuning.kernel("fps_mid") == 256 and tuning.kernel("dense_lds") == 0
     with tuning.override(fps_mid=384):
-        assert tuning.effective_pipeline_profile() == {"dense_lds": 0, "bq_waves": 0}
+        assert tuning.effective_pipeline_profile() == {"dense_lds": 0, "bq_waves": 0, "dense_pair": 0}
         with tuning.pipeline_profile():
             assert tuning.kernel("fps_mid") == 384 and tuning.kernel("dense_lds") == 0
     with tuning.override(pipe_profile=0):
