@@ -988,7 +988,7 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
     (void)A;
     PN2_DSTAMP(0);
     extern __shared__ __attribute__((aligned(16))) char psm[];
-    unsigned *smax = reinterpret_cast<unsigned *>(psm);  // [NW] layer-0 tile maxima
+    unsigned *smax = reinterpret_cast<unsigned *>(psm);  // [NW] layer-0 tile maxima, [NW] A maxima
     char *planes = psm + 64;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1016,7 +1016,8 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
     // for all of it); layer 1's scale still lacks the activation down-scale (dense_alpha's last
     // factor)
     const int col0 = 32 * wave + r, col1 = 32 * t1 + r;
-    const float al0 = dense_alpha<NP0>(A0, col0, 1.f), be0 = A0.raw ? 0.f : A0.beta[col0];
+    const float pa0 = NP0 == 2 ? (A0.raw ? 1.f : A0.alpha[col0]) * A0.wscale[col0] : dense_alpha<NP0>(A0, col0, 1.f);
+    const float be0 = A0.raw ? 0.f : A0.beta[col0];
     const float pa1 = NP1 == 2 ? (A1.raw ? 1.f : A1.alpha[col1]) * A1.wscale[col1] : dense_alpha<NP1>(A1, col1, 1.f);
     const float be1 = A1.raw ? 0.f : A1.beta[col1];
 
@@ -1050,11 +1051,33 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
 #pragma unroll
     for (int i = 0; i < RD; ++i)
         if (i < kb0n) wb[i] = load_wfrag<NP0>(w0 + i * 64, plane0);
+    // NP0 = 2 (split fp16 first layer): the block's scale from the max |value| of its 32 rows'
+    // [xyz | features] -- the unfused layer's dense_act_scale, reduced here over the waves'
+    // k-blocks through LDS (rows past M are copies of row M - 1, which is in the block)
+    ActScale asc0{1.f, 1.f};
+    if constexpr (NP0 == 2) {
+        unsigned m = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+            if (wave + NW * i < kb0n)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m = max(m, abs_bits(xa[i][j]));
+        m = wave_max_u32(m);
+        unsigned *amax = smax + NW;
+        if (lane == 0) amax[wave] = m;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stage_barrier();
+        m = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) m = max(m, amax[i]);
+        asc0 = act_scale(__uint_as_float(m));
+    }
+    const float al0 = NP0 == 2 ? pa0 * asc0.down : pa0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int kb = wave + NW * i;
         if (kb < kb0n) {
-            const Split sp = splitN<NP0>(xa[i]);
+            const Split sp = split_scaled<NP0>(xa[i], asc0.up);
             bf16x8 *dst = reinterpret_cast<bf16x8 *>(planes + kb * NP0 * 1024) + lane;
             dst[0] = sp.h;
             if (NP0 >= 2) dst[64] = sp.m;
@@ -1190,7 +1213,8 @@ static bool dense_pair_ok(const DenseSplitArgs &A0, const DenseSplitArgs &A1, in
         return false;
     if (!A0.vec || !A0.feat || A0.D <= 0 || A0.D % 16 != 0 || A0.kb != 1 + A0.D / 16 || A0.C > 16) return false;
     if (A0.fn % 4 || A0.fb % 4 || ((uintptr_t)A0.feat & 15)) return false;
-    if (np0 != 3 || (np1 != 2 && np1 != 3)) return false;
+    if ((np0 != 3 && np0 != 2) || (np1 != 2 && np1 != 3) || (np0 == 2 && np1 != 2)) return false;
+    if (np0 == 2 && !A0.wscale) return false;
     if (A0.kb != 17 && A0.kb != 41) return false;  // the instantiated k-block counts (D = 256, 640)
     if (np1 == 2 && !A1.wscale) return false;
     if (A1.frag_in) return false;
@@ -1206,12 +1230,15 @@ static void launch_pair(const DenseSplitArgs &A0, const DenseSplitArgs &A1, int 
     hipLaunchKernelGGL((dense_pair_kernel<NP0, NP1, KB0>), grid, block, lds, st, A0, A1, cs);
 }
 
-static int launch_dense_pair(const DenseSplitArgs &A0, const DenseSplitArgs &A1, int np1, hipStream_t st) {
+static int launch_dense_pair(const DenseSplitArgs &A0, const DenseSplitArgs &A1, int np0, int np1, hipStream_t st) {
     const int cs = A1.tiles / kPairWaves;
     const int64_t nrb = (A0.M + 31) / 32;
-    const size_t lds = dense_pair_lds(A0, A1, 3, np1);
+    const size_t lds = dense_pair_lds(A0, A1, np0, np1);
     const dim3 grid((unsigned)(nrb * cs)), block(64 * kPairWaves);
-    if (np1 == 2) {
+    if (np0 == 2) {
+        if (A0.kb == 17) launch_pair<2, 2, 17>(A0, A1, cs, grid, block, lds, st);
+        else launch_pair<2, 2, 41>(A0, A1, cs, grid, block, lds, st);
+    } else if (np1 == 2) {
         if (A0.kb == 17) launch_pair<3, 2, 17>(A0, A1, cs, grid, block, lds, st);
         else launch_pair<3, 2, 41>(A0, A1, cs, grid, block, lds, st);
     } else {
@@ -1463,7 +1490,7 @@ int try_launch_dense_split(const pn2_sa_src &s, const pn2_mlp_layer *layers, int
             DenseSplitArgs B = args_of(1);
             B.frag_in = 0;  // its input never leaves the CU
             if (dense_pair_ok(A, B, layer_np(0), layer_np(1))) {
-                const int rc = launch_dense_pair(A, B, layer_np(1), st);
+                const int rc = launch_dense_pair(A, B, layer_np(0), layer_np(1), st);
                 if (rc != PN2_OK) return rc;
                 flops[layer_np(1)] += layers[1].cin * layers[1].cout;
                 l = 1;

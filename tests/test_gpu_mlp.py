@@ -309,7 +309,7 @@ DENSE_PAIR = [
 ]
 
 
-@pytest.mark.parametrize("f16", [1, 0])
+@pytest.mark.parametrize("f16", [2, 1, 0])
 @pytest.mark.parametrize("lds", [1, 0])
 @pytest.mark.parametrize("case", range(len(DENSE_PAIR)))
 def test_dense_pair_bit_identical(case, lds, f16):
