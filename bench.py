@@ -257,7 +257,8 @@ def load_mfma_busy(cfg):
             d = json.load(fh).get(cfg, {})
     except (OSError, ValueError):
         return None
-    mlp = {k: v for k, v in d.items() if "sa_chain_kernel" in k or "dense_split_kernel" in k}
+    mlp = {k: v for k, v in d.items()
+           if any(n in k for n in ("sa_chain_kernel", "dense_split_kernel", "dense_lds_kernel", "dense_pair_kernel"))}
     if not mlp:
         return None
     t = sum(v["gui_us"] * v["calls"] for v in mlp.values())

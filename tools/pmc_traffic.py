@@ -24,7 +24,7 @@ CALLS_PER_FORWARD = {"ssg": 3, "msg": 7, "pose": 6, "stress": 3}
 FORWARD_MARKER = "fps_kernel"  # one launch per sampled SA layer, counted below
 # kernels one pn2_sa_mlp_max_f32 call may dispatch
 MLP_KERNELS = ("sa_mlp_kernel", "dense_layer_kernel", "sa_chain_kernel", "dense_split_kernel",
-               "dense_lds_kernel", "compact_scan_kernel", "u_table_kernel", "unkey_kernel")
+               "dense_lds_kernel", "dense_pair_kernel", "compact_scan_kernel", "u_table_kernel", "unkey_kernel")
 FPS_PER_FORWARD = {"ssg": 2, "msg": 2, "pose": 3, "stress": 2}
 # pn2_ball_query_f32 calls per forward (one per radius of every grouping SA layer)
 BQ_PER_FORWARD = {"ssg": 2, "msg": 6, "pose": 3, "stress": 2}
