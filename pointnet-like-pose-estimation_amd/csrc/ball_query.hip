@@ -165,19 +165,41 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
             unsigned wd[NR];
 #pragma unroll
             for (int rr = 0; rr < NR; ++rr) wd[rr] = 0;
-            if (np == 32) {
+            if (np == 32 && CC == 0) {  // runtime C (small shapes): one record at a time
 #pragma unroll 8
                 for (int i = 0; i < 32; ++i) {
-                    const float4 *tp = tile + (w * TS + 32 * t + i) * (CP / 4);  // uniform address
                     float pv[CP];
-#pragma unroll
-                    for (int v = 0; v < CP / 4; ++v) {
-                        const float4 q4 = tp[v];
-                        pv[4 * v] = q4.x; pv[4 * v + 1] = q4.y; pv[4 * v + 2] = q4.z; pv[4 * v + 3] = q4.w;
-                    }
+                    point_rec(w * TS + 32 * t + i, pv);
                     const float d = bq_dist<CP>(c, ssq_c, pv, C, small);
 #pragma unroll
-                    for (int rr = 0; rr < NR; ++rr) bq_insert(wd[rr], d, O.r2[rr]);  // point base+i -> bit 31-i
+                    for (int rr = 0; rr < NR; ++rr) bq_insert(wd[rr], d, O.r2[rr]);
+                }
+            } else if (np == 32) {
+                // records in chunks of U points, the next chunk's reads issued before this
+                // chunk's arithmetic (bq_insert's asm keeps the compiler from hoisting them
+                // itself: one read in flight, its full LDS latency per point)
+                constexpr int U = CP == 4 ? 8 : 4;
+                const float4 *tw = tile + (w * TS + 32 * t) * (CP / 4);  // uniform addresses
+                float pv[2][U][CP];
+                auto read_chunk = [&](int k, float (&dst)[U][CP]) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+#pragma unroll
+                        for (int v = 0; v < CP / 4; ++v) {
+                            const float4 q4 = tw[(k * U + u) * (CP / 4) + v];
+                            dst[u][4 * v] = q4.x; dst[u][4 * v + 1] = q4.y; dst[u][4 * v + 2] = q4.z; dst[u][4 * v + 3] = q4.w;
+                        }
+                };
+                read_chunk(0, pv[0]);
+#pragma unroll
+                for (int k = 0; k < 32 / U; ++k) {
+                    if (k + 1 < 32 / U) read_chunk(k + 1, pv[(k + 1) & 1]);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const float d = bq_dist<CP>(c, ssq_c, pv[k & 1][u], C, small);
+#pragma unroll
+                        for (int rr = 0; rr < NR; ++rr) bq_insert(wd[rr], d, O.r2[rr]);  // point base+i -> bit 31-i
+                    }
                 }
             } else if (np > 0) {
                 for (int i = 0; i < 32; ++i) {
