@@ -1096,12 +1096,13 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
     // per k-block, in this order (sched_barrier: the scheduler would sink the weight requests
     // under the MFMAs and leave one or two in flight): the next k-block's A planes from LDS,
     // this k-block's MFMAs, the request RD k-blocks ahead into the register just consumed
-    Split xn = ring_readN<NP0>(planes, lane);
+    Split xb[2];  // A planes double-buffered in registers (static indices: the loop is unrolled)
+    xb[0] = ring_readN<NP0>(planes, lane);
 #pragma unroll
     for (int kb = 0; kb < kb0n; ++kb) {
-        const Split xs = xn;
-        if (kb + 1 < kb0n) xn = ring_readN<NP0>(planes + (kb + 1) * NP0 * 1024, lane);
-        acc = mma_wb<NP0>(xs, wb[kb % RD], acc);
+        if (kb + 1 < kb0n) xb[(kb + 1) & 1] = ring_readN<NP0>(planes + (kb + 1) * NP0 * 1024, lane);
+        __builtin_amdgcn_sched_barrier(0);  // the reads first: a full k-block of MFMAs to land
+        acc = mma_wb<NP0>(xb[kb & 1], wb[kb % RD], acc);
         if (kb + RD < kb0n) wb[kb % RD] = load_wfrag<NP0>(w0 + (int64_t)(kb + RD) * 64, plane0);
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -1169,12 +1170,13 @@ __global__ __launch_bounds__(64 * kPairWaves) void dense_pair_kernel(const Dense
     // ---- 4. layer 1, tile t1
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-    Split yn = ring_readN<NP1>(planes, lane);
+    Split yb[2];
+    yb[0] = ring_readN<NP1>(planes, lane);
 #pragma unroll
     for (int kb = 0; kb < kb1n; ++kb) {
-        const Split xs = yn;
-        if (kb + 1 < kb1n) yn = ring_readN<NP1>(planes + (kb + 1) * NP1 * 1024, lane);
-        acc = mma_wb<NP1>(xs, wc[kb % RD], acc);
+        if (kb + 1 < kb1n) yb[(kb + 1) & 1] = ring_readN<NP1>(planes + (kb + 1) * NP1 * 1024, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        acc = mma_wb<NP1>(yb[kb & 1], wc[kb % RD], acc);
         if (kb + RD < kb1n) wc[kb % RD] = load_wfrag<NP1>(w1 + (int64_t)(kb + RD) * 64, plane1);
         __builtin_amdgcn_sched_barrier(0);
     }
