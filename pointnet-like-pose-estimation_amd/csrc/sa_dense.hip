@@ -952,7 +952,9 @@ static int launch_dense_lds_tile(int tile, const DenseSplitArgs &A, int np, hipS
 // around 5-7 us of stages (tools/debug/dense_stamps.py SEL=1008 / 16).
 // Workgroup = one 32-row block x one of `cs` column slices of the second layer, 8 waves:
 //   1. the block's layer-0 A operand split once into LDS planes [kb][NP0][64 lanes][16 B]
-//      (wave w splits k-blocks w, w + 8, ...);
+//      (wave w loads all of its k-blocks w, w + 8, ... at once, then splits them; NP0 = 2, the
+//      split-fp16 first layer of dense_f16 = 2: after the block's scale is reduced over the
+//      waves through LDS);
 //   2. wave w: layer-0 column tile w over every k-block, its weight fragments streamed straight
 //      into registers RD k-blocks ahead (nothing else to share: each wave has its own tile);
 //   3. BN + ReLU in registers; the block's max |value| (the maxima the unfused layer 0 would
