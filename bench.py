@@ -77,6 +77,8 @@ DEFAULT_PRECISION = {"stress": "bf16"}
 # batches) needs two geometry streams (116k vs 108-111k clouds/s with one); the others are
 # faster with one geometry stream and a tail stream for the heads.
 DEFAULT_GEOMETRY_STREAMS = {"stress": 2}
+# batch slots of the graphed pipeline (at least 4 per geometry group)
+DEFAULT_SLOTS = 8
 
 
 def parse():
@@ -105,10 +107,20 @@ def parse():
     ap.add_argument("--compute-streams", type=int, default=None,
                     help="graphed pipeline: consecutive batches' forwards alternate between this "
                          "many compute streams (1 or 2; default 2 with shared CUs)")
-    ap.add_argument("--geometry-batches", type=int, default=4,
+    ap.add_argument("--geometry-batches", type=int, default=1,
                     help="graphed pipeline: consecutive batches whose geometry (FPS + ball "
-                         "queries) runs as one replay over their clouds side by side, and (tuning "
-                         "pipe_fuse) whose forward runs as one")
+                         "queries) runs as one replay over their clouds side by side (default 1: "
+                         "every launch of the headline value is one B-cloud batch)")
+    ap.add_argument("--fuse", action="store_true",
+                    help="graphed pipeline: one forward (sa + head graphs) per geometry group, "
+                         "its batches side by side (launches of geometry-batches x B clouds)")
+    ap.add_argument("--fused-batches", type=int, default=4,
+                    help="after the headline, the same K batches through a pipeline that fuses "
+                         "this many consecutive batches into every launch (value_fused, "
+                         "launch_batch = this x B); 0 skips it")
+    ap.add_argument("--no-reference-head", action="store_true",
+                    help="skip eager_value_reference_head (the unchanged reference head's "
+                         "forward through the drop-in, pn2.heads.ReferenceForward)")
     ap.add_argument("--geometry-streams", type=int, default=None,
                     help="graphed pipeline: 2 = consecutive groups' FPS chains on two streams "
                          "(default 2 for --config stress, else 1)")
@@ -415,14 +427,17 @@ def main():
         # come in the same order and every head's geometry overlaps every head's MLPs
         pmodel = eager_models[0] if len(eager_models) == 1 else MultiHead(
             eager_models, [i for i, n in enumerate(names) if n.startswith("translation")])
+        def graphed(gb, fuse, nslots=None):
+            return GraphedPipeline(pmodel, geometry_cus=a.geometry_cus,
+                                   tail=not a.no_tail,
+                                   nslots=nslots if nslots is not None else max(4 * gb, DEFAULT_SLOTS),
+                                   geometry_streams=(a.geometry_streams if a.geometry_streams is not None
+                                                     else DEFAULT_GEOMETRY_STREAMS.get(a.config, 1)),
+                                   geometry_batches=gb, fuse=fuse,
+                                   compute_streams=a.compute_streams)
+
         if not a.eager_pipeline:
-            pf = GraphedPipeline(pmodel, geometry_cus=a.geometry_cus,
-                                 tail=not a.no_tail,
-                                 nslots=a.slots if a.slots is not None else 4 * a.geometry_batches,
-                                 geometry_streams=(a.geometry_streams if a.geometry_streams is not None
-                                                   else DEFAULT_GEOMETRY_STREAMS.get(a.config, 1)),
-                                 geometry_batches=a.geometry_batches,
-                                 compute_streams=a.compute_streams)
+            pf = graphed(a.geometry_batches, a.fuse, a.slots)
         else:
             pf = PipelinedForward(pmodel, geometry_cus=a.geometry_cus,
                                   tail="auto" if a.tail else False)
@@ -440,14 +455,15 @@ def main():
             return [h[0] if isinstance(h, tuple) else h for h in o]
         return o[0] if isinstance(o, tuple) else o
 
-    def run_pipelined(k):
+    def run_pipelined(k, pf_=None):
+        pf_ = pf_ or pf
         with shard.batch_shard(gB, lo):
             if a.gather_every > 1:  # one collective per gather_every batches
                 bg = shard.BatchedGather(a.gather_every, total=k)
                 post = lambda i, o: bg(i, first_outputs(o))  # noqa: E731
             else:
                 post = gather
-            pf.run([x] * k, [(mean,)] * k if takes_mean else None, post=post)
+            pf_.run([x] * k, [(mean,)] * k if takes_mean else None, post=post)
 
     for _ in range(max(a.warmup, 2) if a.graph else a.warmup):  # graph: 1st call captures
         step(names, models, x, mean, gB, lo)
@@ -466,7 +482,7 @@ def main():
         t0 = time.perf_counter()
         if pipe:
             kt = None
-            run_pipelined(k)
+            run_pipelined(k, pipe if pipe is not True else None)
         elif timer:
             with ops.kernel_timer() as kt:
                 for _ in range(k):
@@ -505,6 +521,23 @@ def main():
         el_s = max_over_ranks(el_s)
         settled = {"value": round(gB * a.steps / el_s, 2), "ms_per_step": round(el_s / a.steps * 1e3, 4),
                    "settle": "~80 ms of untimed pipelined batches before the same K timed steps"}
+    # The same K batches through a pipeline that fuses `fused_batches` consecutive batches into
+    # every launch (FPS over their clouds side by side, one forward over all their rows): a
+    # serving mode with launch batch fused_batches x B, bit-equal per batch to the eager forward
+    # (tests/test_gpu_configs.py), reported beside the headline, never as it.
+    fused = None
+    if pipelined and not a.eager_pipeline and a.fused_batches > 1 and (
+            a.fuse is False or a.geometry_batches != a.fused_batches):
+        pf4 = graphed(a.fused_batches, True)
+        run_pipelined(max(a.warmup, 2), pf4)
+        run_pipelined(max(a.steps, int(80.0 / max(ms, 1e-3)) + 1), pf4)
+        el_f, _ = timed(a.steps, False, pipe=pf4)
+        el_f = max_over_ranks(el_f)
+        fused = {"value": round(gB * a.steps / el_f, 2), "ms_per_step": round(el_f / a.steps * 1e3, 4),
+                 "launch_batch": a.fused_batches * (hi - lo), "geometry_batches": a.fused_batches,
+                 "launch": "graphed pipeline; %d consecutive batches per launch (FPS, ball queries, "
+                           "MLPs, head), after ~80 ms of untimed batches" % a.fused_batches}
+        del pf4
     if a.graph or pipelined:
         # the eager pass's own warm-up: after the pipelined runs (whose graphs keep private
         # memory pools) the first eager forwards allocate afresh
@@ -512,6 +545,18 @@ def main():
             step(names, eager_models, x, mean, gB, lo)
         el_e, _ = timed(a.steps, False, eager_models)
         eager_value = gB * a.steps / max_over_ranks(el_e)
+    # The unchanged reference head through the drop-in: its forward restated call for call
+    # (pn2.heads.ReferenceForward -- SA modules one after the other, no FPS side job, the torch
+    # FC tail), eager, the same K steps
+    ref_value = None
+    if not a.no_reference_head:
+        from pn2 import heads as _heads
+        if all(n in _heads.HEADS for n in names):
+            ref_models = [_heads.ReferenceForward(m) for m in eager_models]
+            for _ in range(3):
+                step(names, ref_models, x, mean, gB, lo)
+            el_r, _ = timed(a.steps, False, ref_models)
+            ref_value = round(gB * a.steps / max_over_ranks(el_r), 2)
     kt = None
     if not a.no_kernel_timer:
         _, kt = timed(a.steps, True, eager_models)
@@ -595,6 +640,7 @@ def main():
                     "random-init weights and BN statistics (eval mode)" % (
                         " + 7-way one-hot" if kind == "onehot10" else ""),
             "config": {"workload": desc, "global_batch": gB, "points": N, "heads": names,
+                       "launch_batch": (hi - lo) * (a.geometry_batches if pipelined and a.fuse else 1),
                        "parallelism": "dp%d" % world + (" (all_gather forced through RCCL)"
                                                          if a.force_rccl else "")},
             "roofline": roof, "roofline_ball_query": roof_bq, "cpu_baseline": cpu, "kernels": kernels,
@@ -614,6 +660,8 @@ def main():
                            if not a.eager_pipeline else "")
                        if pipelined else "eager"),
             "eager_value": round(eager_value, 2),
+            "eager_value_reference_head": ref_value,
+            "value_fused": fused,
             "value_settled": settled,
             # hardware queues of this process (bench.py sets 8 unless --hw-queues 0; HIP's own
             # default is 4: DESIGN.md §6)

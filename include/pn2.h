@@ -75,12 +75,14 @@ const char *pn2_last_error(void);
  *                            index_points raises IndexError); the SA kernels read point 0 there
  *   PN2_DEVERR_INDEX         pn2_index_points_f32 / pn2_group_f32 got an index outside [-N, N)
  *                            (the element is NaN)
+ * A launch raises into the slot of the device its STREAM belongs to (hipStreamGetDevice; the
+ * current device for the null stream), whatever the thread's current device is.
  * pn2_error_slot_set(slot): from now on, launches by the calling thread on the current device
  * raise into `slot` -- two caller-owned, zeroed uint32 DEVICE words ([0] the bits, [1] scratch
  * for the take) that must outlive every launch and captured graph that uses them (a graph
  * raises into the slot of the thread that captured it).  NULL: back to the process-wide
  * default slot, which every thread without a slot of its own shares.
- * pn2_error_slot_take: the calling thread's slot (on the current device), taken -- read and,
+ * pn2_error_slot_take: the calling thread's slot on `stream`'s device, taken -- read and,
  * when `clear` != 0, reset in ONE device atomic, so a bit raised meanwhile is never lost --
  * stream-ordered on `stream`, which it then waits for.
  * pn2_device_errors: the same take after hipDeviceSynchronize (every stream's work done).

@@ -310,7 +310,7 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
     }
     const int64_t rb_kb = tuning().bq_rowbuf_kb < 96 ? tuning().bq_rowbuf_kb : 96;
     const bool rowbuf = obytes <= (size_t)rb_kb * 1024;
-    unsigned *err = error_word();
+    unsigned *err = error_word(st);
     PN2_REQUIRE(err, "pn2_ball_query_f32: no device error slot");
 #define PN2_BQ_L2(NW, PP, RB)                                                                          \
     do {                                                                                               \

@@ -60,10 +60,23 @@ static int current_device(int *dev) {
     return PN2_OK;
 }
 
-unsigned *error_word() {
-    int d = 0;
-    if (hipGetDevice(&d) == hipSuccess && d >= 0 && d < kMaxDevices && t_slots[d]) return t_slots[d];
-    return default_error_slot();
+// the device a launch on `st` runs on: the stream's own device (a model on cuda:1 may be
+// launched while the thread's current device is cuda:0), the current one for the null stream
+int stream_device(hipStream_t st) {
+    int d = -1;
+    if (st) {
+        hipDevice_t sd = -1;
+        if (hipStreamGetDevice(st, &sd) == hipSuccess) d = (int)sd;
+    }
+    if (d < 0 && hipGetDevice(&d) != hipSuccess) return -1;
+    return d >= 0 && d < kMaxDevices ? d : -1;
+}
+
+unsigned *error_word(hipStream_t st) {
+    const int d = stream_device(st);
+    if (d < 0) return nullptr;
+    if (t_slots[d]) return t_slots[d];
+    return default_error_slot(d);
 }
 
 // take (and with clear, reset) `slot`, stream-ordered on st, then wait for st
@@ -79,7 +92,7 @@ static int take(unsigned *slot, int clear, uint32_t *bits, hipStream_t st, bool 
         return true;
     };
     bool ok;
-    if (slot == default_error_slot()) {  // shared with other threads: one reader at a time
+    if (is_default_error_slot(slot)) {  // shared with other threads: one reader at a time
         std::lock_guard<std::mutex> g(g_default_read);
         ok = run();
     } else {
@@ -113,14 +126,16 @@ extern "C" int pn2_error_slot_set(uint32_t *slot) {
 
 extern "C" int pn2_error_slot_take(int clear, uint32_t *bits, void *stream) {
     PN2_REQUIRE(bits, "pn2_error_slot_take: null pointer");
-    if (!pn2::default_error_slot()) return pn2::set_error(PN2_EHIP, "pn2_error_slot_take: no default slot");
-    return pn2::take(pn2::error_word(), clear, bits, pn2::as_stream(stream), false);
+    unsigned *slot = pn2::error_word(pn2::as_stream(stream));
+    if (!slot) return pn2::set_error(PN2_EHIP, "pn2_error_slot_take: no device error slot");
+    return pn2::take(slot, clear, bits, pn2::as_stream(stream), false);
 }
 
 extern "C" int pn2_device_errors(int clear, uint32_t *bits) {
     PN2_REQUIRE(bits, "pn2_device_errors: null pointer");
-    if (!pn2::default_error_slot()) return pn2::set_error(PN2_EHIP, "pn2_device_errors: no default slot");
-    return pn2::take(pn2::error_word(), clear, bits, nullptr, true);
+    unsigned *slot = pn2::error_word(nullptr);
+    if (!slot) return pn2::set_error(PN2_EHIP, "pn2_device_errors: no device error slot");
+    return pn2::take(slot, clear, bits, nullptr, true);
 }
 
 extern "C" int pn2_tuning_get(const char *key, int64_t *value) {

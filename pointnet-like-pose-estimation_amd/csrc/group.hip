@@ -21,18 +21,31 @@ namespace pn2 {
 // the process-wide default error slot (pn2_internal.h): [0] bits, [1] the take's snapshot
 __device__ unsigned g_default_errors[2];
 
-unsigned *default_error_slot() {
-    static std::atomic<unsigned *> cache[kMaxDevices];
-    int d = 0;
-    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDevices) return nullptr;
-    unsigned *p = cache[d].load(std::memory_order_acquire);
+static std::atomic<unsigned *> g_default_cache[kMaxDevices];
+
+// device d's copy of g_default_errors (the symbol's address is per device: resolved with d
+// current, once)
+unsigned *default_error_slot(int d) {
+    if (d < 0 || d >= kMaxDevices) return nullptr;
+    unsigned *p = g_default_cache[d].load(std::memory_order_acquire);
     if (!p) {
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+        if (cur != d && hipSetDevice(d) != hipSuccess) return nullptr;
         void *a = nullptr;
-        if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_default_errors)) != hipSuccess) return nullptr;
+        const hipError_t e = hipGetSymbolAddress(&a, HIP_SYMBOL(g_default_errors));
+        if (cur != d) (void)hipSetDevice(cur);
+        if (e != hipSuccess) return nullptr;
         p = static_cast<unsigned *>(a);
-        cache[d].store(p, std::memory_order_release);
+        g_default_cache[d].store(p, std::memory_order_release);
     }
     return p;
+}
+
+bool is_default_error_slot(const unsigned *slot) {
+    for (int d = 0; d < kMaxDevices; ++d)
+        if (slot && g_default_cache[d].load(std::memory_order_acquire) == slot) return true;
+    return false;
 }
 
 // the slot's value (and, with clear, its reset) in ONE device atomic: a bit that a kernel ORs in
@@ -117,7 +130,7 @@ extern "C" int pn2_index_points_f32(const float *pts, int64_t B, int64_t N, int6
     PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && M >= 0, "pn2_index_points_f32: bad shape");
     const int64_t tot = B * M * C;
     if (tot == 0) return PN2_OK;
-    unsigned *err = error_word();
+    unsigned *err = error_word(as_stream(stream));
     PN2_REQUIRE(err, "pn2_index_points_f32: no device error slot");
     hipLaunchKernelGGL(index_points_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
                        as_stream(stream), pts, B, N, C, sb, sn, sc, idx, M, out, err);
@@ -136,7 +149,7 @@ extern "C" int pn2_group_f32(const float *pts, int64_t B, int64_t N, int64_t C, 
                 "pn2_group_f32: bad shape");
     const int64_t tot = B * S * K * (C + D);
     if (tot == 0) return PN2_OK;
-    unsigned *err = error_word();
+    unsigned *err = error_word(as_stream(stream));
     PN2_REQUIRE(err, "pn2_group_f32: no device error slot");
     hipLaunchKernelGGL(group_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
                        as_stream(stream), pts, N, C, sb, sn, sc, feat, D, fb, fn, fd, ctr, S, idx,

@@ -52,6 +52,8 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
                            /* are written straight to HBM (0: always)                      */ \
     X(fps_threads, 0)      /* FPS block shape threads x points per thread (0: automatic)   */ \
     X(fps_ppt, 0)                                                                              \
+    X(fps_red, 0)          /* FPS cross-wave winner: 0 LDS atomic key, 1 key slots + barrier, */ \
+                           /* 2 tagged key slots, no barrier (fps_body.h RED)                */ \
     X(fps_mid, 512)        /* automatic FPS block for 256 < N <= 1024: 512 threads x 2      */ \
                            /* points (fastest alone: the eager forward) or 256 x 4 (the     */ \
                            /* pipelines' geometry, beside the chains)                       */ \
@@ -76,11 +78,14 @@ struct Tuning {
 Tuning tuning();
 
 // ---- device error slots (pn2_error_slot_set): two device words, [0] the PN2_DEVERR_* bits the
-// kernels OR in, [1] the take kernel's snapshot.  error_word(): the launching thread's slot on
-// the current device, else the process-wide default slot (a __device__ array, group.hip).
+// kernels OR in, [1] the take kernel's snapshot.  error_word(st): the launching thread's slot on
+// the device of the launch stream st (the current device for the null stream), else that
+// device's process-wide default slot (a __device__ array, group.hip).
 constexpr int kMaxDevices = 64;
-unsigned *error_word();
-unsigned *default_error_slot();  // the current device's default slot; nullptr on a HIP error
+int stream_device(hipStream_t st);  // -1 on a HIP error
+unsigned *error_word(hipStream_t st);
+unsigned *default_error_slot(int device);  // nullptr on a HIP error
+bool is_default_error_slot(const unsigned *slot);
 // one device atomic takes slot[0] (and with clear resets it: a bit raised meanwhile is never
 // lost) into slot[1], copied to *bits; stream-ordered on st, which it then waits for
 hipError_t take_errors(unsigned *slot, int clear, unsigned *bits, hipStream_t st);

@@ -239,6 +239,50 @@ class SignMSG(_FCHead):
         return x, torch.sign(x - 0.5)
 
 
+class ReferenceForward(nn.Module):
+    """What the reference's own head file computes through the drop-in: its forward restated
+    call for call -- the SA modules one after the other (no FPS side job: an unchanged
+    reference head never enters ``geometry.fps_ahead``) and the FC tail as the torch modules
+    fc/bn/relu/drop, log_softmax and ``x.data.max(1)[1]``.  Wraps one of the heads above (same
+    parameters); bench.py's ``eager_value_reference_head`` times it.
+
+      pointnet2_cls_ssg.py:22-38, pointnet2_cls_msg.py:22-38, rotation_ssg.py:24-38,
+      rotation_msg.py:24-38, translation_ssg.py:28-44, translation_msg.py:28-44
+    """
+
+    def __init__(self, head):
+        super().__init__()
+        self.head = head
+
+    def _tail(self, x):
+        h = self.head
+        x = h.drop(F.relu(h.bn1(h.fc1(x))))
+        x = h.drop(F.relu(h.bn2(h.fc2(x))))
+        return h.fc3(x)
+
+    def forward(self, points, mean=None):
+        h = self.head
+        B = points.shape[0]
+        if isinstance(h, (TranslationSSG, TranslationMSG)) and h.mean_mlp == 'True':
+            mean = h.mean_fc2(F.relu(h.mean_bn1(h.mean_fc1(mean))))
+        l1p, l1f = h.sa1(points, None)
+        l2p, l2f = h.sa2(l1p, l1f)
+        if hasattr(h, "sa3"):
+            _, feat = h.sa3(l2p, l2f)
+        else:
+            feat = l2f
+        x = self._tail(feat.view(B, 1024))
+        if isinstance(h, (ClsSSG, ClsMSG)):
+            x = F.log_softmax(x, -1)
+            return x, feat, x.data.max(1)[1]
+        if isinstance(h, (TranslationSSG, TranslationMSG)):
+            return x + mean
+        if isinstance(h, (SignSSG, SignMSG)):
+            x = torch.sigmoid(x)
+            return x, torch.sign(x - 0.5)
+        return x
+
+
 HEADS = {
     "pointnet2_cls_ssg": ClsSSG,
     "pointnet2_cls_msg": ClsMSG,
