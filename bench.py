@@ -73,12 +73,13 @@ STRONG = {"pose"}
 # MLP arithmetic per config: BASELINE config 5 (stress) asks for features/MLP in bf16, the
 # others are the reference's fp32
 DEFAULT_PRECISION = {"stress": "bf16"}
-# Geometry streams per config (graphed pipeline): STRESS's N=16384 FPS (~1 ms per group of two
-# batches) needs two geometry streams (116k vs 108-111k clouds/s with one); the others are
-# faster with one geometry stream and a tail stream for the heads.
+# Geometry streams of the graphed pipeline: two at one batch per launch (the headline: each
+# batch's FPS chain is ~280 us of one stream against a ~300 us batch period; SSG K = 20 98-100k
+# vs 93-95k with one); fused launches (value_fused) keep r05's choice per config -- STRESS's
+# N=16384 FPS needs two, the others one with a tail stream for the heads.
 DEFAULT_GEOMETRY_STREAMS = {"stress": 2}
 # batch slots of the graphed pipeline (at least 4 per geometry group)
-DEFAULT_SLOTS = 8
+DEFAULT_SLOTS = 16
 
 
 def parse():
@@ -432,7 +433,8 @@ def main():
                                    tail=not a.no_tail,
                                    nslots=nslots if nslots is not None else max(4 * gb, DEFAULT_SLOTS),
                                    geometry_streams=(a.geometry_streams if a.geometry_streams is not None
-                                                     else DEFAULT_GEOMETRY_STREAMS.get(a.config, 1)),
+                                                     else 2 if gb == 1 else
+                                                     DEFAULT_GEOMETRY_STREAMS.get(a.config, 1)),
                                    geometry_batches=gb, fuse=fuse,
                                    compute_streams=a.compute_streams)
 

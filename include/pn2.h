@@ -62,7 +62,7 @@ extern "C" {
 #define PN2_EUNSUPPORTED (-2) /* shape outside what the kernels are built for */
 #define PN2_EHIP (-3)       /* HIP runtime error at launch */
 
-#define PN2_ABI_VERSION 16
+#define PN2_ABI_VERSION 17
 
 int pn2_abi_version(void);
 const char *pn2_last_error(void);
@@ -415,6 +415,10 @@ int pn2_sa_mlp_last_path(void);
 /* Planes per operand of the MLP kernels of this thread's last successful pn2_sa_mlp_max_* call:
  * 3 (split bf16: 6 MFMAs per product), 2 (split fp16: 3), 1 (bf16), 0 (fp32 MFMA kernels). */
 int pn2_sa_mlp_last_planes(void);
+/* Where this thread's last pn2_sa_mlp_max_* call ran its FPS side job (pn2_sa_src.fps_side):
+ * 1 inside the chain launch (extra workgroups of that launch), 0 as its own launch after the
+ * MLP, -1 the call had no side job (ABI 17). */
+int pn2_sa_mlp_last_fps_side(void);
 
 /* ---- runtime: CU-partitioned streams (pipelined serving, pn2/pipeline.py) ---- */
 int pn2_device_cu_count(int device, int *count);

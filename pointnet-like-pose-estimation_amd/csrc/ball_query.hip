@@ -309,7 +309,13 @@ static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, in
         obytes += (size_t)64 * (O.K[r] + 1) * sizeof(OT);
     }
     const int64_t rb_kb = tuning().bq_rowbuf_kb < 96 ? tuning().bq_rowbuf_kb : 96;
-    const bool rowbuf = obytes <= (size_t)rb_kb * 1024;
+    // the kernel's static LDS for this shape (tile + per-segment counts + first hits): the row
+    // buffer gets what is left of the CU's 160 KB, else the rows go straight to HBM (an MSG
+    // layer's multi-radius launch with long rows would otherwise fail to launch)
+    const int nwe = nw == 1 ? 1 : nw == 2 ? 2 : (CP > 4 ? 2 : 4);
+    const size_t lds_static = (size_t)P * 32 * nwe * CP * 4 + (size_t)2 * NR * P * 64 * 4 + (size_t)NR * 64 * 4;
+    const size_t lds_left = lds_static < (size_t)160 * 1024 ? (size_t)160 * 1024 - lds_static : 0;
+    const bool rowbuf = obytes <= (size_t)rb_kb * 1024 && obytes <= lds_left;
     unsigned *err = error_word(st);
     PN2_REQUIRE(err, "pn2_ball_query_f32: no device error slot");
 #define PN2_BQ_L2(NW, PP, RB)                                                                          \

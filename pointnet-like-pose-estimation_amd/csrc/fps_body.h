@@ -305,33 +305,44 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
             if constexpr (NW == 1) {
                 far = ol * PPT + bj;
             } else if constexpr (RED != 0) {
-                // the wave's key (wave-uniform: wv, ol, bj live in SGPRs) into its slot
+                // the wave's key (wave-uniform: wv, ol, bj live in SGPRs) into its slot, through
+                // an explicit LDS pointer (a volatile access through a generic one is a flat
+                // access: each of them waits for the one before)
+                typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+                typedef __attribute__((address_space(3))) volatile unsigned long long lds_u64;
+                typedef __attribute__((address_space(3))) volatile u64x2 lds_u64x2;
                 const unsigned idx = (unsigned)((wave * 64 + ol) * PPT + bj);
                 const unsigned tag = (unsigned)(i >> 1) & 0xFFFFu;
                 const unsigned lo = RED == 2 ? ((tag << 16) | (0xFFFFu - idx)) : (0xFFFFFFFFu - idx);
-                volatile unsigned long long *sl = key + (i & 1) * NW;
+                unsigned long long *slg = key + (i & 1) * NW;
                 PN2_FPS_T(3);
-                if (lane == 0) sl[wave] = ((unsigned long long)wv << 32) | lo;
+                if (lane == 0) ((lds_u64 *)slg)[wave] = ((unsigned long long)wv << 32) | lo;
                 PN2_FPS_T(4);
+                static_assert(NW % 2 == 0, "key slots are read in pairs");
                 unsigned long long kk[NW];
+                auto read_all = [&]() {
+#pragma unroll
+                    for (int w = 0; w < NW; w += 2) {
+                        const u64x2 v = ((lds_u64x2 *)slg)[w >> 1];  // broadcast ds_read_b128
+                        kk[w] = v.x;
+                        kk[w + 1] = v.y;
+                    }
+                };
                 if constexpr (RED == 1) {
                     __syncthreads();
                     PN2_FPS_T(5);
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) kk[w] = sl[w];
+                    read_all();
                 } else {
                     // every wave's store of this iteration is visible once its tag is: the LDS
                     // runs a wave's operations in order, and a slot of this parity is next
                     // written two iterations on, after its writer has seen every key of the
                     // iteration in between -- i.e. after every wave has read this one
                     for (int spin = 0;; ++spin) {
+                        read_all();
                         bool ok = true;
 #pragma unroll
-                        for (int w = 0; w < NW; ++w) {
-                            kk[w] = sl[w];
-                            ok = ok && (unsigned)(kk[w] >> 16 & 0xFFFFu) == tag;
-                        }
-                        if (ok || spin > (1 << 20)) break;  // bounded: never a hang
+                        for (int w = 0; w < NW; ++w) ok = ok && (unsigned)((kk[w] >> 16) & 0xFFFFu) == tag;
+                        if (ok || spin > (1 << 16)) break;  // bounded: never a hang
                     }
                     PN2_FPS_T(5);
                 }

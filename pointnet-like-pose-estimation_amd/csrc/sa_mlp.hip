@@ -869,6 +869,8 @@ static thread_local int g_last_path = 0;
 static thread_local int g_last_planes = 0;  // planes per operand of the call's MLP kernels
 extern "C" int pn2_sa_mlp_last_path(void) { return g_last_path; }
 extern "C" int pn2_sa_mlp_last_planes(void) { return g_last_planes; }
+static thread_local int g_last_side = -1;  // pn2_sa_mlp_last_fps_side
+extern "C" int pn2_sa_mlp_last_fps_side(void) { return g_last_side; }
 
 // the src's zero side job on the paths whose kernels do not take it (the dense-layer path's
 // last layer does)
@@ -993,7 +995,9 @@ static int with_fps_side(const pn2_sa_src *src, void *stream, F &&mlp) {
     const int rc = mlp();
     const bool taken = fps_side_taken();
     fps_side_taken() = false;
-    if (rc != PN2_OK || !side || taken) return rc;
+    if (rc != PN2_OK) return rc;
+    g_last_side = !side ? -1 : taken ? 1 : 0;
+    if (!side || taken) return rc;
     return fps_side_launch(*side, as_stream(stream));
 }
 

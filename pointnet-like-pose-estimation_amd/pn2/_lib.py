@@ -94,6 +94,7 @@ SIGNATURES = {
     "pn2_layer_split_bytes": (_i64, [_i64, _i64, _i64]),
     "pn2_sa_mlp_last_path": (_int, []),
     "pn2_sa_mlp_last_planes": (_int, []),
+    "pn2_sa_mlp_last_fps_side": (_int, []),
     "pn2_device_cu_count": (_int, [_int, ctypes.POINTER(_int)]),
     "pn2_stream_create_cu_masked": (_int, [_int, ctypes.POINTER(ctypes.c_uint32), _int, ctypes.POINTER(_vp)]),
     "pn2_stream_destroy": (_int, [_vp]),
@@ -131,7 +132,7 @@ SIGNATURES = {
                                _int, _vp, _i64, _vp, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 _lib = None
 
 

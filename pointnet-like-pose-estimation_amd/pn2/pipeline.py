@@ -45,6 +45,7 @@ stream when ``run`` is called.
 """
 import atexit
 import ctypes
+import contextlib
 import os
 import time
 
@@ -231,8 +232,18 @@ class PipelinedForward:
         one after the other.  The copy keeps x's layout (the packed squared norms follow the
         reference's layout-dependent summation order), and every start is still drawn in layer
         order before any launch."""
-        with tuning.pipeline_profile():  # the launch choices measured best beside the chains
+        with self._profile():  # the launch choices measured best beside the chains
             return self._fps_chain_body(x)
+
+    def _profile(self):
+        """The kernel-selection profile of this pipeline's launches: tuning.PIPELINE_PROFILE
+        where it was measured best (the eager pipeline, and graphed pipelines that fuse several
+        batches into every launch), else the eager forward's defaults (the graphed pipeline at
+        one batch per launch: its launches are the eager forward's, and there the eager forms
+        read 104-112k vs 97-100k clouds/s, SSG K = 20, interleaved x3)."""
+        if getattr(self, "use_profile", True):
+            return tuning.pipeline_profile()
+        return contextlib.nullcontext()
 
     def _fps_chain_body(self, x):
         B, _, N = x.shape
@@ -310,7 +321,7 @@ class PipelinedForward:
         if use_tail and self.sas:
             handle = self.sas[-1].register_forward_hook(self._to_tail(tail))
         try:
-            with tuning.pipeline_profile():
+            with self._profile():
                 self._run(batches, extras, post, geo, main, outs)
         finally:
             if handle is not None:
@@ -514,6 +525,7 @@ class GraphedPipeline(PipelinedForward):
                              not tuning.get("heads_on_compute"))  # A/B
         self.nslots = int(nslots)
         self.gb = gb
+        self.use_profile = self.fuse and gb > 1  # see PipelinedForward._profile
         self.ngroups = self.nslots // gb
         self.geometry_streams = int(geometry_streams)
         self.trace = None
@@ -621,7 +633,7 @@ class GraphedPipeline(PipelinedForward):
         """New sa / head graphs for every batch slot after a parameter change (their kernels
         read the parameters' memory); the geometry graphs read only coordinates and draws, and
         are kept."""
-        with tuning.pipeline_profile():
+        with self._profile():
             for grp in self._slots:
                 B = grp.B
                 grp.halves = self._group_forwards(
@@ -703,7 +715,7 @@ class GraphedPipeline(PipelinedForward):
                 outs = self._run_eager(batches[:1], None if extras is None else extras[:1],
                                        post, False)
             self._draws = draws
-            with tuning.pipeline_profile():
+            with self._profile():
                 self._slots = [self._capture(batches[0], extra_of(0), dev, draws)
                                for _ in range(self.ngroups)]
             self._key = sig

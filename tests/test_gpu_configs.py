@@ -2,7 +2,7 @@
 
 Kernel choices depend on the batch (dense tile widths via dense_minwg, 256 x 128 tiles at >= 512
 workgroups, the XCD remap when the workgroup count is a multiple of 8, the compact pool modes,
-FPS over a geometry group of 2 batches in the pipeline), so the reduced-batch goldens do not
+FPS over a geometry group of 4 batches in the fused pipeline), so the reduced-batch goldens do not
 cover the configs' own launches.  Here each config runs at its batch:
 
   msg     pointnet2_cls_msg  B=32  N=4096     (pointnet2_cls_msg.py:22-38)
@@ -19,7 +19,9 @@ bar).  Features are checked for every cloud where the float64 MLP takes seconds 
 for 33 clouds spread over the batch at stress (every 4th and the last; the oracle's bf16
 emulation of all 128 takes minutes) -- there every cloud's features are also checked against a
 torch restatement of the bf16 arithmetic on the GPU (same bar); indices for every cloud everywhere.  The same batch through pn2.pipeline.GraphedPipeline
-(geometry groups of 2 batches, graphs on their streams) must give the eager outputs bit for bit.
+(one batch per launch, and four batches fused per launch; graphs on their streams) must give the
+eager outputs bit for bit, and so must POSE's per-rank shape (global B=64 over 8 ranks: B=8, with
+the batch_shard draws) through both launches, shard by shard.
 """
 import itertools
 
@@ -204,11 +206,13 @@ def test_config_full_batch_vs_oracle(cfg):
     assert next(d, None) is None
 
 
+@pytest.mark.parametrize("gb,fuse", [(1, False), (4, True)])
 @pytest.mark.parametrize("cfg", sorted(CONFIGS))
-def test_config_full_batch_pipeline_equals_eager(cfg, monkeypatch):
-    """GraphedPipeline (the bench's launch: geometry of 2 batches per FPS launch, 2 compute
-    streams, the heads on the tail stream) over 4 batches with the eager pass's start draws:
-    every batch's outputs equal the eager outputs bit for bit."""
+def test_config_full_batch_pipeline_equals_eager(cfg, gb, fuse, monkeypatch):
+    """GraphedPipeline -- the bench's headline launch (one batch per launch, 2 compute streams,
+    the heads on the tail stream) and its value_fused launch (4 consecutive batches fused into
+    every launch) -- over 4 batches with the eager pass's start draws: every batch's outputs
+    equal the eager outputs bit for bit."""
     import pn2
     from pn2 import shard
     from pn2.pipeline import GraphedPipeline, MultiHead
@@ -233,7 +237,8 @@ def test_config_full_batch_pipeline_equals_eager(cfg, monkeypatch):
     takes_mean = any(n.startswith("translation") for n in names)
     n = 4
     with torch.no_grad(), pn2.mlp_precision(prec):
-        gp = GraphedPipeline(model, geometry_streams=2 if cfg == "stress" else 1)
+        gp = GraphedPipeline(model, geometry_streams=2 if cfg == "stress" else 1, geometry_batches=gb,
+                             fuse=fuse, nslots=max(8, 4 * gb))
         outs = gp.run([xd] * n, [(md,)] * n if takes_mean else None)
     torch.cuda.synchronize()
     want = eager[0] if len(models) == 1 else tuple(eager)
@@ -249,3 +254,55 @@ def _flat(o):
     if isinstance(o, torch.Tensor):
         return [o]
     return [t for x in o for t in _flat(x)]
+
+
+@pytest.mark.parametrize("gb,fuse", [(1, False), (4, True)])
+def test_pose_rank_shards_pipeline_equals_unsharded(gb, fuse, monkeypatch):
+    """BASELINE config 4 at the shape each of 8 ranks runs (rotation_ssg.py:24-38,
+    translation_ssg.py:28-44): global B=64 sharded 8 ways is B=8 per rank, and each rank's
+    GraphedPipeline (one batch per launch, or four fused into each launch: 32-cloud launches)
+    draws the FULL batch's FPS starts and keeps its slice (shard.batch_shard).  Every shard's
+    outputs, for every pipelined batch, equal its rows of the unsharded eager forward bit for
+    bit."""
+    import pn2
+    from pn2 import shard
+    from pn2.pipeline import GraphedPipeline, MultiHead
+    names, models, x, mean, prec, _ = _build("pose")
+    B, N, W = x.shape[0], x.shape[2], 8
+    torch.manual_seed(57)
+    draws = _draws(names, models, B, N)
+    xd, md = x.to(DEV), mean.to(DEV)
+    state = {"i": 0}
+
+    def full_draw(N_):
+        t = draws[state["i"] % len(draws)]
+        state["i"] += 1
+        assert int(t.max()) < N_
+        return t
+
+    torch.manual_seed(57)
+    eager = _forward(names, models, xd, md, prec)  # the reference's unsharded draws, in order
+    flat_w = _flat(tuple(eager))
+    model = MultiHead(models, [i for i, n in enumerate(names) if n.startswith("translation")])
+    n = 4
+    for r in range(W):
+        lo, hi = shard.shard_range(B, r, W)
+        state["i"] = 0
+
+        def fixed_draw(B_, N_, pin=True, lo=lo):
+            assert B_ == hi - lo
+            return full_draw(N_)[lo:lo + B_].clone()
+
+        monkeypatch.setattr(shard, "draw_start", fixed_draw)
+        monkeypatch.setattr(shard, "draw_start_into", lambda dst, N_: dst.copy_(fixed_draw(dst.shape[0], N_)))
+        with torch.no_grad(), pn2.mlp_precision(prec), shard.batch_shard(B, lo):
+            gp = GraphedPipeline(model, geometry_batches=gb, fuse=fuse, nslots=max(8, 4 * gb))
+            outs = gp.run([xd[lo:hi]] * n, [(md[lo:hi],)] * n)
+        torch.cuda.synchronize()
+        del gp
+        for i, o in enumerate(outs):
+            flat_o = _flat(o)
+            assert len(flat_o) == len(flat_w)
+            for a, b in zip(flat_o, flat_w):
+                np.testing.assert_array_equal(a.cpu().numpy(), b[lo:hi].cpu().numpy(),
+                                              err_msg="rank %d batch %d" % (r, i))

@@ -38,6 +38,17 @@ def test_fps_ahead_matches_plain_forward(head, C, N, side):
     model = model.to(DEV).eval()
     B = 6
     x = cases.cloud("onehot10" if C == 10 else "uniform3", B, N, 22).permute(0, 2, 1).contiguous().to(DEV)
+    from pn2 import _lib
+    where = []
+    hk = model.sa1.register_forward_hook(lambda *a: where.append(_lib.load().pn2_sa_mlp_last_fps_side()))
+    with torch.no_grad(), tuning.override(fps_side=side):
+        torch.manual_seed(5)
+        got = model(x)
+    hk.remove()
+    # where sa1's MLP call ran sa2's FPS: inside the chain launch (the N = 512 centroid clouds
+    # of the SSG heads fit the chain's side-job block) or, with fps_side = 0, as its own launch
+    if head in ("pointnet2_cls_ssg", "rotation_ssg"):
+        assert where == [1 if side else 0]
     with torch.no_grad(), tuning.override(fps_side=side):
         torch.manual_seed(5)
         got = model(x)
@@ -76,6 +87,7 @@ def test_fps_side_job_direct():
             job, outs = ops.fps_side_job(side_pts, S2, st)
             out = torch.empty_like(ref)
             ops.sa_mlp_max_impl(out, 0, pts, None, newp, idx, wts, als, bes, cins, splits, cnt=cnt, fps_side=job)
+            assert pn2._lib.load().pn2_sa_mlp_last_fps_side() == (1 if n2 == 512 else 0)
             want = ops.fps_direct(side_pts, S2, st)
             for a, b in zip(outs, want):
                 assert torch.equal(a, b)

@@ -192,7 +192,7 @@ def test_batched_gather_matches_per_batch(B, world, every):
 BENCH = os.path.join(os.path.dirname(PKG), "bench.py")
 
 
-@pytest.mark.parametrize("config,gpus", [("ssg", 2), ("pose", 3)])
+@pytest.mark.parametrize("config,gpus", [("ssg", 2), ("pose", 3), ("pose", 8)])
 def test_bench_launcher_plumbing(config, gpus):
     """`bench.py --gpus N` (no torchrun) starts N ranks itself with the torchrun environment;
     --plumbing-check runs their gloo group, shard split and uneven all_gather on the CPU (pose:

@@ -1,7 +1,7 @@
 """Is the pipelined SSG run host-bound?  For K batches: the host time run() takes to issue
 everything (it returns before the GPU is done) against the whole run's time (to the final
 synchronize), and the same with the bench's `post` (the per-batch logits gather).
-    python tools/debug/host_bound.py"""
+    python tools/debug/host_bound.py [geometry_batches fuse slots geometry_streams]"""
 import os
 import sys
 import time
@@ -25,7 +25,11 @@ def main():
     cases.randomize_bn(model, 8)
     model = model.to(DEV)
     x = cases.cloud("uniform3", 32, 1024, 90).permute(0, 2, 1).contiguous().to(DEV)
-    gp = GraphedPipeline(model)
+    a = [int(v) for v in sys.argv[1:5]] + [None] * 4
+    gb = a[0] or 1
+    gp = GraphedPipeline(model, geometry_batches=gb, fuse=bool(a[1]) if a[1] is not None else None,
+                         nslots=a[2] or max(8, 4 * gb), geometry_streams=a[3] or 1)
+    print("geometry_batches %d fuse %s slots %d geometry_streams %d" % (gb, gp.fuse, gp.nslots, gp.geometry_streams))
 
     def post(i, o):
         return shard.all_gather_rows(o[0], sizes="shard")

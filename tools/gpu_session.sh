@@ -3,7 +3,7 @@
 #   PYTEST=all (optional: the whole -m gpu suite first) or PYTEST_K="expr" (a -k selection)
 #   KT="tag:tuning|tag:tuning" (optional: eager rocprofv3 kernel traces per PN2_TUNING variant,
 #                                summarised by tools/kstats.py)
-#   VARIANTS=... (optional: interleaved bench A/B, tools/args_ab.sh syntax), STEPS, WARMUP, ROUNDS
+#   VARIANTS=... (optional: interleaved bench A/B, tools/ab.sh syntax), STEPS, WARMUP, ROUNDS
 #   BENCH_ARGS=... (passed to every bench run)
 # Every GPU step has its own time limit; the first failure ends the script.
 set -u
@@ -29,5 +29,5 @@ if [ -n "${KT:-}" ]; then
   done
 fi
 if [ -n "${VARIANTS:-}" ]; then
-  bash tools/args_ab.sh || exit $?
+  bash tools/ab.sh || exit $?
 fi
