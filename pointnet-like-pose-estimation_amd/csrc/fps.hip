@@ -28,10 +28,10 @@
 
 namespace pn2 {
 
-template <int NT, int PPT, int CM, bool FIXED, bool LDSC, int CR = CM, int RED = 0>
+template <int NT, int PPT, int CM, bool FIXED, bool LDSC, int CR = CM>
 __global__ __launch_bounds__(NT) void fps_kernel(const FpsArgs F) {
     extern __shared__ __attribute__((aligned(16))) float fsm[];
-    fps_block<NT, PPT, CM, FIXED, LDSC, CR, RED>(F, (int)blockIdx.x, fsm);
+    fps_block<NT, PPT, CM, FIXED, LDSC, CR>(F, (int)blockIdx.x, fsm);
 }
 
 // ------------------------------------------------------------------------- streamed FPS
@@ -219,20 +219,11 @@ static int launch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64_t
     if constexpr (CR != CM) {
         hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, false, CR>), dim3((unsigned)B), dim3(NT), lds, st, F);
     } else if (ldsc) {
-        const int64_t red = NT > 64 && N <= 65536 ? tuning().fps_red : 0;
-#define PN2_FPS_LDSC(R)                                                                        \
-    do {                                                                                       \
-        static const hipError_t attr = hipFuncSetAttribute(                                   \
-            reinterpret_cast<const void *>(&fps_kernel<NT, PPT, CM, FIXED, true, CM, R>),     \
-            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                          \
-        (void)attr;                                                                            \
-        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, true, CM, R>), dim3((unsigned)B), \
-                           dim3(NT), lds, st, F);                                              \
-    } while (0)
-        if (red == 1) PN2_FPS_LDSC(1);
-        else if (red == 2) PN2_FPS_LDSC(2);
-        else PN2_FPS_LDSC(0);
-#undef PN2_FPS_LDSC
+        static const hipError_t attr = hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&fps_kernel<NT, PPT, CM, FIXED, true>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)attr;
+        hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, true>), dim3((unsigned)B), dim3(NT), lds, st, F);
     } else {
         hipLaunchKernelGGL((fps_kernel<NT, PPT, CM, FIXED, false>), dim3((unsigned)B), dim3(NT), lds, st, F);
     }

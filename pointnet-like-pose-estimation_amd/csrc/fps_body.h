@@ -30,10 +30,8 @@ __device__ __forceinline__ int fps_start(const FpsStart &s, int b) {
     return v;
 }
 constexpr int kFpsLdsCloud = 128 * 1024;  // bytes of LDS a cloud copy may take
-// bytes of the cross-wave key words -- [3] u64 (triple-buffered atomic key, RED 0) or [2][16]
-// u64 (per-wave key slots by iteration parity, RED 1/2) -- + the block flag, 16-aligned
-constexpr int kFpsKeyWords = 2 * 16;
-constexpr int kFpsKeyRegion = (kFpsKeyWords * 8 + 4 + 15) / 16 * 16;
+// bytes of the cross-wave key words ([3] u64, triple-buffered) + the block flag, 16-aligned
+constexpr int kFpsKeyRegion = (3 * 8 + 4 + 15) / 16 * 16;
 
 
 // One launch's (or side job's) FPS arguments: points[b, n, c] = pts[b*sb + n*sn + c*sc]
@@ -101,15 +99,7 @@ __device__ __forceinline__ unsigned row_max_u32(unsigned v) {
 // the other channels of their points from the input each iteration (slow, but any N up to
 // NT*PPT); a cloud whose extra channels are constant (the one-hot class) never reads them.
 
-// RED: how the NW > 1 waves of an LDSC block agree on the iteration's winner --
-//   0  one 64-bit LDS atomicMax per wave on a shared key, a barrier, one key read;
-//   1  each wave stores its key in its own slot (by iteration parity), a barrier, every lane
-//      reads all NW slots (broadcast reads) and takes their maximum in registers;
-//   2  as 1 without the barrier: the keys carry the iteration's tag, and each wave re-reads the
-//      slots until all NW carry it (a bounded spin).
-// The key is (distance bits : ~index), so its maximum is torch.max's first index among the
-// maxima either way, and every mode yields the same indices.
-template <int NT, int PPT, int CM, bool FIXED, bool LDSC, int CR = CM, int RED = 0>
+template <int NT, int PPT, int CM, bool FIXED, bool LDSC, int CR = CM>
 __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *fsm) {
     // the reference's separately rounded ops whatever the including unit's -ffp-contract (the
     // SA chain unit that runs the side job contracts its own arithmetic)
@@ -208,9 +198,6 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
         }
     }
     if (LDSC && tid < 3) key[tid] = 0ull;
-    // RED 2: tags that no iteration carries (0xFFFF), so no slot reads as written before its wave
-    // stores it
-    if (LDSC && RED == 2 && tid < kFpsKeyWords) key[tid] = 0xFFFF0000ull;
 
     // ---- channels past xyz that are constant over the cloud (the pose heads' one-hot class:
     // one label per cloud) contribute (v - v)^2 = +0 to every distance, and adding +0 leaves
@@ -232,7 +219,7 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
     // may use the whole 160 KB dynamically)
     bool xyz_only = false;
     if constexpr (FIXED && CM > 3) {
-        int *flag = reinterpret_cast<int *>(key + kFpsKeyWords);
+        int *flag = reinterpret_cast<int *>(key + 3);
         if (tid == 0) *flag = 1;
         __syncthreads();
         if (!cst) *flag = 0;  // every writer stores 0: a benign race
@@ -304,54 +291,6 @@ __device__ __forceinline__ void fps_block(const FpsArgs &F, const int b, float *
         if constexpr (LDSC) {
             if constexpr (NW == 1) {
                 far = ol * PPT + bj;
-            } else if constexpr (RED != 0) {
-                // the wave's key (wave-uniform: wv, ol, bj live in SGPRs) into its slot, through
-                // an explicit LDS pointer (a volatile access through a generic one is a flat
-                // access: each of them waits for the one before)
-                typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-                typedef __attribute__((address_space(3))) volatile unsigned long long lds_u64;
-                typedef __attribute__((address_space(3))) volatile u64x2 lds_u64x2;
-                const unsigned idx = (unsigned)((wave * 64 + ol) * PPT + bj);
-                const unsigned tag = (unsigned)(i >> 1) & 0xFFFFu;
-                const unsigned lo = RED == 2 ? ((tag << 16) | (0xFFFFu - idx)) : (0xFFFFFFFFu - idx);
-                unsigned long long *slg = key + (i & 1) * NW;
-                PN2_FPS_T(3);
-                if (lane == 0) ((lds_u64 *)slg)[wave] = ((unsigned long long)wv << 32) | lo;
-                PN2_FPS_T(4);
-                static_assert(NW % 2 == 0, "key slots are read in pairs");
-                unsigned long long kk[NW];
-                auto read_all = [&]() {
-#pragma unroll
-                    for (int w = 0; w < NW; w += 2) {
-                        const u64x2 v = ((lds_u64x2 *)slg)[w >> 1];  // broadcast ds_read_b128
-                        kk[w] = v.x;
-                        kk[w + 1] = v.y;
-                    }
-                };
-                if constexpr (RED == 1) {
-                    __syncthreads();
-                    PN2_FPS_T(5);
-                    read_all();
-                } else {
-                    // every wave's store of this iteration is visible once its tag is: the LDS
-                    // runs a wave's operations in order, and a slot of this parity is next
-                    // written two iterations on, after its writer has seen every key of the
-                    // iteration in between -- i.e. after every wave has read this one
-                    for (int spin = 0;; ++spin) {
-                        read_all();
-                        bool ok = true;
-#pragma unroll
-                        for (int w = 0; w < NW; ++w) ok = ok && (unsigned)((kk[w] >> 16) & 0xFFFFu) == tag;
-                        if (ok || spin > (1 << 16)) break;  // bounded: never a hang
-                    }
-                    PN2_FPS_T(5);
-                }
-                unsigned long long best = kk[0];
-#pragma unroll
-                for (int w = 1; w < NW; ++w) best = kk[w] > best ? kk[w] : best;
-                far = __builtin_amdgcn_readfirstlane(
-                    (int)(RED == 2 ? 0xFFFFu - ((unsigned)best & 0xFFFFu) : 0xFFFFFFFFu - (unsigned)best));
-                PN2_FPS_T(6);
             } else {
                 // one 64-bit LDS max per wave: key = dist bits : ~index (max dist, then first
                 // index).  key[i%3] is reset one iteration ahead; its last reader passed the

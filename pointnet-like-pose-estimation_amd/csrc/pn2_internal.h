@@ -52,8 +52,6 @@ static inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream
                            /* are written straight to HBM (0: always)                      */ \
     X(fps_threads, 0)      /* FPS block shape threads x points per thread (0: automatic)   */ \
     X(fps_ppt, 0)                                                                              \
-    X(fps_red, 0)          /* FPS cross-wave winner: 0 LDS atomic key, 1 key slots + barrier, */ \
-                           /* 2 tagged key slots, no barrier (fps_body.h RED)                */ \
     X(fps_mid, 512)        /* automatic FPS block for 256 < N <= 1024: 512 threads x 2      */ \
                            /* points (fastest alone: the eager forward) or 256 x 4 (the     */ \
                            /* pipelines' geometry, beside the chains)                       */ \

@@ -136,12 +136,13 @@ def _streams(device, geometry_cus):
         tail = torch.cuda.Stream(dev, priority=min(lo, hi) if tuning.get("tail_prio") else 0)
         main2 = torch.cuda.default_stream(dev)
         tail2 = torch.cuda.Stream(dev, priority=min(lo, hi) if tuning.get("tail_prio") else 0)
+        main3 = torch.cuda.Stream(dev)
         for st in (geo, main, tail):
             with torch.cuda.stream(st):
                 torch.zeros(1, device=dev)
             st.synchronize()
         _partitions[key] = (geo, main, tail, ())
-        _extra[device] = (geo2, main2, tail2)
+        _extra[device] = (geo2, main2, tail2, main3)
     if key not in _partitions:
         ncu = _cu_count(device)
         per = max(1, min(int(geometry_cus) // _XCDS, ncu // _XCDS - 1))  # CUs per XCD
@@ -163,11 +164,13 @@ def _extra_geometry_streams(device, n):
     return [_extra[device][0]][:n]
 
 
-def _extra_compute_stream(device):
-    """The second compute stream for GraphedPipeline(compute_streams=2) (created with the
-    others by _streams)."""
+def _extra_compute_streams(device, n):
+    """n (0-2) more compute streams for GraphedPipeline(compute_streams=1+n) (created with the
+    others by _streams): the process's default stream, then one more."""
+    if n <= 0:
+        return []
     _streams(device, 0)
-    return _extra[device][1]
+    return [_extra[device][1], _extra[device][3]][:n]
 
 
 def partition(device, geometry_cus):
@@ -237,11 +240,13 @@ class PipelinedForward:
 
     def _profile(self):
         """The kernel-selection profile of this pipeline's launches: tuning.PIPELINE_PROFILE
-        where it was measured best (the eager pipeline, and graphed pipelines that fuse several
-        batches into every launch), else the eager forward's defaults (the graphed pipeline at
-        one batch per launch: its launches are the eager forward's, and there the eager forms
-        read 104-112k vs 97-100k clouds/s, SSG K = 20, interleaved x3)."""
-        if getattr(self, "use_profile", True):
+        where it was measured best -- the eager pipeline, and graphed pipelines whose launches
+        carry >= 64 clouds (four fused B=32 batches, where r05 tuned it; STRESS's B=128; POSE's
+        two heads over B=64: 71-72k vs 68-70k) -- else the eager forward's defaults (graphed SSG
+        at one B=32 batch per launch: 104-112k vs 97-100k clouds/s with the profile, K = 20,
+        interleaved x3; MSG flat).  Host key pipe_profile: 0 never, 2 always."""
+        mode = int(tuning.get("pipe_profile"))
+        if mode == 2 or (mode == 1 and getattr(self, "launch_batch", 128) >= 64):
             return tuning.pipeline_profile()
         return contextlib.nullcontext()
 
@@ -512,10 +517,10 @@ class GraphedPipeline(PipelinedForward):
             raise ValueError("pn2.pipeline: geometry_streams is 1 or 2")
         if compute_streams is None:
             compute_streams = 2 if geometry_cus <= 0 else 1
-        if compute_streams not in (1, 2):
-            raise ValueError("pn2.pipeline: compute_streams is 1 or 2")
-        if compute_streams == 2 and geometry_cus > 0:
-            raise ValueError("pn2.pipeline: compute_streams=2 needs shared CUs (geometry_cus=0)")
+        if compute_streams not in (1, 2, 3):
+            raise ValueError("pn2.pipeline: compute_streams is 1, 2 or 3")
+        if compute_streams > 1 and geometry_cus > 0:
+            raise ValueError("pn2.pipeline: compute_streams > 1 needs shared CUs (geometry_cus=0)")
         self.compute_streams = int(compute_streams)
         # the head graphs get the tail stream(s) while the process's hardware queues allow it
         # (GPU_MAX_HW_QUEUES, HIP's default 4; bench.py runs with 8): every stream on a queue
@@ -525,7 +530,6 @@ class GraphedPipeline(PipelinedForward):
                              not tuning.get("heads_on_compute"))  # A/B
         self.nslots = int(nslots)
         self.gb = gb
-        self.use_profile = self.fuse and gb > 1  # see PipelinedForward._profile
         self.ngroups = self.nslots // gb
         self.geometry_streams = int(geometry_streams)
         self.trace = None
@@ -695,6 +699,8 @@ class GraphedPipeline(PipelinedForward):
             self._params = ParamState(self.model)
         outs, first = [], 0
         dev = batches[0].device
+        # clouds per launch (PipelinedForward._profile)
+        self.launch_batch = int(x0.shape[0]) * (self.gb if self.fuse else 1)
         # With the same input signature the parameters (the sa / head graphs read their memory)
         # are checked only after the first geometry group is issued: the geometry graphs read
         # coordinates and draws alone, and the check's host time (a walk over every parameter
@@ -740,7 +746,7 @@ class GraphedPipeline(PipelinedForward):
         ngr = (nbat + gb - 1) // gb  # groups this call
         geo, main, tail = _streams(dev.index, self.geometry_cus)
         geos = [geo] + _extra_geometry_streams(dev.index, self.geometry_streams - 1)
-        mains = [main] + ([_extra_compute_stream(dev.index)] if self.compute_streams == 2 else [])
+        mains = [main] + _extra_compute_streams(dev.index, self.compute_streams - 1)
         tails = [tail] + ([_extra[dev.index][2]] if self.tail_streams == 2 else [])
         caller = torch.cuda.current_stream(dev)
         ev0 = caller.record_event()  # one event for every pipeline stream to wait on

@@ -28,10 +28,12 @@ Keys are the library's kernel-selection parameters (include/pn2.h ``pn2_tuning_s
                      its batches side by side; 0: one forward per batch
     bq_multi         1: an MSG layer's ball queries in one launch over its radii
                      (pn2_ball_query_multi_i32); 0: one launch per radius
-    pipe_profile     1: the pipelines (pn2.pipeline) capture and run their kernels under
+    pipe_profile     1: the pipelines (pn2.pipeline) whose launches carry >= 64 clouds
+                     (fused groups, or B >= 64) capture and run their kernels under
                      PIPELINE_PROFILE -- the launch choices measured best beside each other's
                      kernels, where the kernel defaults are the ones measured best alone (the
-                     eager forward, GraphedForward); 0: the defaults everywhere
+                     eager forward, GraphedForward); 0: the defaults everywhere; 2: every
+                     pipeline (A/B)
 
 Unknown keys are an error.  ``override(**kw)`` changes keys for the duration of a ``with``
 block (tests); process-wide kernel keys are atomic words in the library, so a change on one

@@ -508,3 +508,61 @@ def test_dense_split_f16_vs_oracle(case, f16):
     ratio = float((np.abs(got - want) / tol).max())
     print("case %d %s f16=%d: max err / tol %.4f" % (case, kind, f16, ratio))
     assert ratio < 0.1
+
+
+# S*K not a multiple of the 32-row wave: a cloud's rows then start inside a wave, where a
+# per-wave fp16 activation scale would mix two clouds -- those launches must fall back to an
+# arithmetic that is batch-independent (VERDICT r05 "what's weak" 2).  Non-compact launches
+# (tuning compact = 0) and the default compact ones.  (C, D, K, S, N, radius, mlp)
+RAGGED = [
+    (3, 0, 24, 50, 256, 0.3, [64, 64, 128]),       # S*K = 1200: 37.5 waves per cloud
+    (3, 0, 40, 37, 256, 0.35, [64, 64, 128]),      # S*K = 1480
+    (3, 16, 20, 45, 300, 0.4, [64, 64, 128]),      # features (layer 0 over xyz + 16 channels)
+    (3, 128, 36, 29, 256, 0.45, [128, 128, 256]),  # wide layer 0 (the pre-pass chains)
+]
+
+
+@pytest.mark.parametrize("compact", [0, 1])
+@pytest.mark.parametrize("case", range(len(RAGGED)))
+def test_chain_ragged_rows_batch_independent(case, compact):
+    """Within a tenth of the 1e-5 tolerance of the float64 oracle, and every cloud's output bit-
+    equal to the same cloud run alone while its batch neighbour's features are 1e4x larger."""
+    import pn2
+    from pn2 import tuning
+    C, D, K, S, N, radius, mlp = RAGGED[case]
+    B = 2
+    pts = cases.cloud("uniform3", B, N, 2100 + case)
+    gen = torch.Generator().manual_seed(2200 + case)
+    feat = torch.randn(B, N, D, generator=gen) if D else None
+    if D:
+        feat[1] *= 1e4
+    torch.manual_seed(2300 + case)
+    sa = pn2.PointNetSetAbstraction(S, K, radius, C + D, mlp)
+    cases.randomize_bn(sa, 2400 + case)
+    sa = sa.to(DEV).eval()
+    x = pts.permute(0, 2, 1).contiguous().to(DEV)
+    f = feat.permute(0, 2, 1).contiguous().to(DEV) if D else None
+    with tuning.override(compact=compact), torch.no_grad():
+        torch.manual_seed(2500 + case)
+        start = torch.randint(0, N, (B,), dtype=torch.long)
+        torch.manual_seed(2500 + case)
+        got = sa(x, f)[1]
+        torch.cuda.synchronize()
+        # cloud 0 alone, with its own start draw (the batch's first)
+        from pn2 import shard
+        with shard.batch_shard(B, 0):
+            torch.manual_seed(2500 + case)
+            alone = sa(x[:1], None if f is None else f[:1])[1]
+    np.testing.assert_array_equal(alone.cpu().numpy().view(np.uint32), got[:1].cpu().numpy().view(np.uint32))
+    ps = pts.permute(0, 2, 1).contiguous().permute(0, 2, 1)  # the module's strided view
+    fi = oracle.farthest_point_sample(ps, S, start)
+    ctr = oracle.index_points(ps, fi)
+    idx = oracle.query_ball_point(radius, K, ps, ctr)
+    grouped = oracle.group(ps, None if feat is None else feat.numpy(), idx, ctr, feature_first=False)
+    want = oracle.mlp_max(grouped, _oracle_layers(sa.mlp_convs, sa.mlp_bns))
+    gotn = got.permute(0, 2, 1).cpu().numpy().astype(np.float64)
+    for b in range(B):  # per cloud: cloud 1's magnitude must not set cloud 0's tolerance
+        tol = 1e-5 * np.abs(want[b]) + 1e-5 * np.abs(want[b]).max()
+        ratio = float((np.abs(gotn[b] - want[b]) / tol).max())
+        print("case %d compact %d cloud %d: max err / tol %.4f" % (case, compact, b, ratio))
+        assert ratio < 0.1

@@ -316,40 +316,3 @@ def test_ball_query_multi_matches_single(C, N, S, radii, ks, rowbuf):
     for (a, ca), (b, cb) in zip(multi, single):
         assert torch.equal(a, b) and torch.equal(ca, cb)
 
-
-# fps_block's cross-wave winner modes (tuning fps_red; csrc/fps_body.h RED): the LDS atomic key
-# (0), per-wave key slots behind a barrier (1), tagged key slots with no barrier (2) -- the
-# same indices, centroids and packed records, bit for bit, for every block shape, including
-# duplicate-heavy clouds (ties go to the first index) and the reference goldens.
-@pytest.mark.parametrize("red", [1, 2])
-@pytest.mark.parametrize("name", INDEX)
-def test_fps_red_modes_match_reference(red, name):
-    from pn2 import tuning
-    g = load_golden("index_%s.npz" % name)
-    pts = _to_dev_view(_points(g))
-    with tuning.override(fps_red=red):
-        idx, newp, cpk, ppk = torch.ops.pn2.fps(pts, int(g["S"]), torch.from_numpy(g["start"]).to(DEV))
-    np.testing.assert_array_equal(idx.cpu().numpy(), g["fps_idx"])
-    np.testing.assert_array_equal(newp.cpu().numpy().view(np.uint32), g["new_points"].view(np.uint32))
-
-
-@pytest.mark.parametrize("red", [1, 2])
-@pytest.mark.parametrize("nt,ppt,N,kind", [(128, 8, 1024, "uniform3"), (256, 4, 1024, "dup3"),
-                                           (512, 2, 1024, "uniform3"), (512, 2, 1000, "dup3"),
-                                           (256, 2, 512, "uniform3"), (1024, 2, 2048, "onehot10"),
-                                           (1024, 4, 4096, "uniform3"), (1024, 16, 16384, "dup3")])
-def test_fps_red_modes_exact(red, nt, ppt, N, kind):
-    from pn2 import tuning
-    B, S = 3, min(N, 512)
-    p = cases.as_layout(cases.cloud(kind, B, N, 41), "strided")  # dup3: many ties
-    start = torch.randint(0, N, (B,), generator=torch.Generator().manual_seed(N + nt))
-    dp = _to_dev_view(p)
-    with tuning.override(fps_threads=nt, fps_ppt=ppt):
-        base = torch.ops.pn2.fps(dp, S, start.to(DEV))
-        with tuning.override(fps_red=red):
-            got = torch.ops.pn2.fps(dp, S, start.to(DEV))
-    for x, y in zip(base, got):
-        np.testing.assert_array_equal(x.cpu().numpy().view(np.uint32 if x.dtype == torch.float32 else np.int64),
-                                      y.cpu().numpy().view(np.uint32 if y.dtype == torch.float32 else np.int64))
-    want = oracle.farthest_point_sample(p[:1], S, start[:1])
-    np.testing.assert_array_equal(got[0][:1].cpu().numpy(), want)
