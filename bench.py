@@ -1,33 +1,37 @@
 """Throughput benchmark: point-clouds/sec of the pointnet2_cls_ssg forward (eval), B=32 clouds
 of N=1024 points per GPU, on the MI355X-native SA path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ssg|msg|pose|stress]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ssg|msg|pose|stress|v1]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 One step = one forward of the head over every rank's batch shard (weak scaling: B clouds per
 GPU, global batch = B*N) followed by the RCCL all_gather of the logits -- the only exchange the
-data-parallel path has.  Single-head configs run the K steps through
-pn2.pipeline.GraphedPipeline (the FPS chain of step i+1 on its own stream while step i's ball
-queries and MLPs run, the head on a third stream, every stage replayed from HIP graphs; every
-step computes exactly the eager forward, with the same CPU-RNG draws); --eager-pipeline issues
-the same pipeline op by op, --no-pipeline runs the steps one after the other, --graph replays
-each as one HIP graph.  Inputs are
-resident in HBM before the timed region, which carries no instrumentation.  Rank 0 prints one
-JSON line (contract in the task statement) with:
-  value         clouds/s of the timed region; eager_value is the same K steps run one after
-                the other, op by op.
+data-parallel path has.  Inputs are resident in HBM before the timed region, which carries no
+instrumentation.  Rank 0 prints one JSON line (contract in the task statement) with:
+  value         clouds/s of K steps through pn2.pipeline.GraphedPipeline with EVERY LAUNCH ONE
+                B-cloud BATCH (geometry_batches=1, fuse=False): independent B=32 forwards
+                overlapped on streams -- each batch's geometry (FPS + ball queries) replayed from a
+                HIP graph on one of two geometry streams, its SA forward on a compute stream, its
+                head on a tail stream; every step computes exactly its eager forward, with the
+                same CPU-RNG draws.  --no-pipeline times plain eager steps instead, --graph whole-
+                forward HIP-graph replays.
+  value_fused   the same K batches through a pipeline that fuses --fused-batches (4) consecutive
+                batches into every launch (launch_batch = 4 x B): a serving mode, not the metric.
+  eager_value   the same K steps one after the other, op by op (B / forward time).
+  eager_value_reference_head
+                the same, through pn2.heads.ReferenceForward: the reference head's forward
+                restated call for call (pointnet2_cls_ssg.py:22-38), i.e. what the unchanged
+                reference caller gets through the drop-in.
   roofline      dominant op = pn2_sa_mlp_max_f32 (gather + shared MLP + max; sa_chain_kernel /
-                dense_split_kernel): achieved = algorithmic fp32 FLOPs (2*M*sum(cin*cout) per
-                call, cin unpadded) / call duration timed with HIP events on the launch stream,
-                over a further K eager steps (kernel durations are launch-mode independent;
-                profiles/ has the rocprofv3 check).  The products are fp32-accurate splits on the
-                16-bit matrix cores: split fp16 (3 MFMAs per fp32 product) in the chains, split
-                bf16 (6) in the dense layers, so peak = the flops-weighted ceiling of that mix,
-                from the fp16/bf16 dense MFMA peak 2516.8 TFLOP/s: /3 = 838.9, /6 = 419.5
-                (MI355X_MICROARCH.md; the 157.3 TFLOP/s fp32 MFMA peak is reported beside it,
-                and frac_vs_split_bf16_ceiling for comparison with earlier rounds).  traffic = HBM bytes
-                per call from rocprofv3 PMC (profiles/pmc_traffic.json, FETCH_SIZE x2 +
-                WRITE_SIZE, per MI355X_MICROARCH.md) when present for this config, else null.
+                dense_*_kernel): achieved = algorithmic fp32 FLOPs (2*M*sum(cin*cout) per call,
+                cin unpadded) / call duration timed with HIP events on the launch stream, over a
+                further K eager steps (profiles/ has the rocprofv3 check).  The products are
+                fp32-accurate splits on the 16-bit matrix cores (split fp16: 3 MFMAs per fp32
+                product; split bf16: 6), so peak = the flops-weighted ceiling of the mix the calls
+                ran, from the fp16/bf16 dense MFMA peak 2516.8 TFLOP/s (MI355X_MICROARCH.md).
+                traffic = HBM bytes per call from rocprofv3 PMC (profiles/pmc_traffic.json).
+  roofline_ball_query
+                query_ball_point, the north star's named kernel: VALU-bound, HBM fraction beside.
   cpu_baseline  oracle/torch_ref.py -- the reference's formulation in torch-CPU ops -- timed on
                 this host's cores on a bounded sample (rank 0, N=1 only).
 """
