@@ -77,10 +77,15 @@ STRONG = {"pose"}
 # MLP arithmetic per config: BASELINE config 5 (stress) asks for features/MLP in bf16, the
 # others are the reference's fp32
 DEFAULT_PRECISION = {"stress": "bf16"}
-# Geometry streams of the graphed pipeline: two at one batch per launch (the headline: each
-# batch's FPS chain is ~280 us of one stream against a ~300 us batch period; SSG K = 20 98-100k
-# vs 93-95k with one); fused launches (value_fused) keep r05's choice per config -- STRESS's
-# N=16384 FPS needs two, the others one with a tail stream for the heads.
+# Geometry streams of the graphed pipeline.  At one batch per launch (the headline) each
+# batch's FPS chain takes ~550-650 us of its stream under the compute kernels' contention
+# (tools/debug/gpipe_events.py) against a ~270 us batch period, so four geometry streams, and
+# the ball queries run in each batch's forward on the compute streams (SSG K = 20: 121-123k vs
+# 96-110k with two streams and the queries on the geometry streams); with the geometry off the
+# critical path the heads' tail stream backs up, so consecutive heads alternate between two tail
+# streams (119.8-121.9k; 8 hardware queues: 4 geometry + 2 compute + 2 tail).  Fused launches
+# (value_fused) keep r05's choice per config -- STRESS's N=16384 FPS needs two, the others one
+# with a tail stream for the heads.
 DEFAULT_GEOMETRY_STREAMS = {"stress": 2}
 # batch slots of the graphed pipeline (at least 4 per geometry group)
 DEFAULT_SLOTS = 16
@@ -129,6 +134,9 @@ def parse():
     ap.add_argument("--geometry-streams", type=int, default=None,
                     help="graphed pipeline: 2 = consecutive groups' FPS chains on two streams "
                          "(default 2 for --config stress, else 1)")
+    ap.add_argument("--geometry-bq", type=int, choices=(0, 1), default=None,
+                    help="graphed pipeline: 1 = the ball queries on the geometry streams after each "
+                         "FPS, 0 = in each batch's forward (default 0 at one batch per launch)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="plain eager steps (default for single-head configs: pn2.pipeline)")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default=None,
@@ -433,14 +441,18 @@ def main():
         pmodel = eager_models[0] if len(eager_models) == 1 else MultiHead(
             eager_models, [i for i, n in enumerate(names) if n.startswith("translation")])
         def graphed(gb, fuse, nslots=None):
+            one = gb == 1 or not fuse  # every launch one batch (the headline)
             return GraphedPipeline(pmodel, geometry_cus=a.geometry_cus,
                                    tail=not a.no_tail,
                                    nslots=nslots if nslots is not None else max(4 * gb, DEFAULT_SLOTS),
                                    geometry_streams=(a.geometry_streams if a.geometry_streams is not None
-                                                     else 2 if gb == 1 else
+                                                     else 4 if one else
                                                      DEFAULT_GEOMETRY_STREAMS.get(a.config, 1)),
                                    geometry_batches=gb, fuse=fuse,
-                                   compute_streams=a.compute_streams)
+                                   compute_streams=a.compute_streams,
+                                   geometry_bq=(bool(a.geometry_bq) if a.geometry_bq is not None
+                                                else False if one else None),
+                                   tail_streams=2 if one else None)
 
         if not a.eager_pipeline:
             pf = graphed(a.geometry_batches, a.fuse, a.slots)
@@ -660,9 +672,10 @@ def main():
                            "; geometry of %d batches per replay" % a.geometry_batches +
                            ("; one forward per geometry group" if getattr(pf, "_slots", None) and
                             pf._slots[0].halves[0].fused else "; one forward per batch") +
-                           ("; %d compute + %d geometry streams%s" % (
-                               pf.compute_streams, pf.geometry_streams,
-                               "" if pf.head_on_tail else ", heads on the compute streams"))
+                           ("; %d compute + %d geometry + %d tail streams%s%s" % (
+                               pf.compute_streams, pf.geometry_streams, pf.tail_streams,
+                               "" if pf.head_on_tail else ", heads on the compute streams",
+                               "; ball queries in each batch's forward" if pf.geometry_bq is False else ""))
                            if not a.eager_pipeline else "")
                        if pipelined else "eager"),
             "eager_value": round(eager_value, 2),

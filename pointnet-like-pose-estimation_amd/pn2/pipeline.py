@@ -154,14 +154,26 @@ def _streams(device, geometry_cus):
     return _partitions[key][:3]
 
 
+_more_geo = {}  # device -> geometry streams past the second (GraphedPipeline(geometry_streams>2))
+
+
 def _extra_geometry_streams(device, n):
-    """n (0 or 1) more high-priority streams for GraphedPipeline(geometry_streams=1+n) (shared
-    CUs; created with the others by _streams).  n = 0 touches no stream: with geometry_cus > 0
-    the shared-CU set would add queues beyond the masked streams'."""
+    """n (0-3) more high-priority streams for GraphedPipeline(geometry_streams=1+n) (shared
+    CUs; the second is created with the others by _streams, later ones on first use).  n = 0
+    touches no stream: with geometry_cus > 0 the shared-CU set would add queues beyond the
+    masked streams'."""
     if n <= 0:
         return []
     _streams(device, 0)
-    return [_extra[device][0]][:n]
+    more = _more_geo.setdefault(device, [])
+    while len(more) < n - 1:
+        lo, hi = torch.cuda.Stream.priority_range()
+        st = torch.cuda.Stream(torch.device("cuda", device), priority=min(lo, hi))
+        with torch.cuda.stream(st):
+            torch.zeros(1, device=torch.device("cuda", device))
+        st.synchronize()
+        more.append(st)
+    return ([_extra[device][0]] + more)[:n]
 
 
 def _extra_compute_streams(device, n):
@@ -272,7 +284,8 @@ class PipelinedForward:
         entries = {}
         # geometry_bq = 0: the ball queries run in each batch's forward instead (the module
         # queries when its entry holds no lists), leaving the FPS alone on the geometry stream
-        bq = bool(tuning.get("geometry_bq"))
+        gbq = getattr(self, "geometry_bq", None)
+        bq = bool(tuning.get("geometry_bq")) if gbq is None else bool(gbq)
         pts = x.permute(0, 2, 1)
         first = {}  # chain -> (newp, cpk, ppk) of its first layer
         heads = [ch[0] for ch in chains]
@@ -482,7 +495,7 @@ class GraphedPipeline(PipelinedForward):
     compute_streams=2 (default with shared CUs): consecutive batches' sa graphs alternate
     between two compute streams, so one batch's short dependent kernels (scans, the pre-pass)
     and its kernels' last partial waves of workgroups run beside the other batch's chains.
-    geometry_streams=2: consecutive groups' geometry replays alternate between two
+    geometry_streams=2..4: consecutive groups' geometry replays alternate between that many
     high-priority streams.  A process gets 4 hardware queues (GPU_MAX_HW_QUEUES): one geometry
     stream + two compute streams + the tail stream is the default; with two geometry streams
     and two compute streams the head graphs run on their batch's compute stream after its sa
@@ -494,8 +507,12 @@ class GraphedPipeline(PipelinedForward):
     """
 
     def __init__(self, model, geometry_cus=0, tail=True, nslots=16, geometry_streams=1,
-                 geometry_batches=4, compute_streams=None, fuse=None):
+                 geometry_batches=4, compute_streams=None, fuse=None, geometry_bq=None,
+                 tail_streams=None):
         super().__init__(model, geometry_cus, bool(tail))
+        # geometry_bq: the ball queries on the geometry streams after each layer's FPS (True),
+        # or in each batch's forward on the compute streams (False); None: tuning geometry_bq
+        self.geometry_bq = geometry_bq
         # fuse: one forward (sa + head graphs) over the whole geometry group -- its gb batches
         # side by side, every launch with gb times the rows -- instead of one per batch.  Each
         # cloud is computed exactly as in its own batch's forward (per-cloud kernels; the FC
@@ -513,8 +530,8 @@ class GraphedPipeline(PipelinedForward):
         # 2 at most: with the compute and tail streams that is the 4 hardware queues a process
         # gets (GPU_MAX_HW_QUEUES); a fifth stream shares a queue and serialises behind another
         # (measured: 3 geometry streams 42.8k clouds/s at SSG vs 76.1k with 2)
-        if geometry_streams not in (1, 2):
-            raise ValueError("pn2.pipeline: geometry_streams is 1 or 2")
+        if geometry_streams not in (1, 2, 3, 4):
+            raise ValueError("pn2.pipeline: geometry_streams is 1 to 4")
         if compute_streams is None:
             compute_streams = 2 if geometry_cus <= 0 else 1
         if compute_streams not in (1, 2, 3):
@@ -525,7 +542,8 @@ class GraphedPipeline(PipelinedForward):
         # the head graphs get the tail stream(s) while the process's hardware queues allow it
         # (GPU_MAX_HW_QUEUES, HIP's default 4; bench.py runs with 8): every stream on a queue
         # of its own
-        self.tail_streams = 2 if int(tuning.get("tail_streams")) == 2 and geometry_cus <= 0 else 1
+        ts = int(tuning.get("tail_streams")) if tail_streams is None else int(tail_streams)
+        self.tail_streams = 2 if ts == 2 and geometry_cus <= 0 else 1
         self.head_on_tail = (geometry_streams + self.compute_streams + self.tail_streams <= _hw_queues() and
                              not tuning.get("heads_on_compute"))  # A/B
         self.nslots = int(nslots)

@@ -237,8 +237,12 @@ def test_config_full_batch_pipeline_equals_eager(cfg, gb, fuse, monkeypatch):
     takes_mean = any(n.startswith("translation") for n in names)
     n = 4
     with torch.no_grad(), pn2.mlp_precision(prec):
-        gp = GraphedPipeline(model, geometry_streams=2 if cfg == "stress" else 1, geometry_batches=gb,
-                             fuse=fuse, nslots=max(8, 4 * gb))
+        # the bench's launches: one batch per launch with four geometry streams and the ball
+        # queries in each batch's forward; four fused batches with r05's geometry streams
+        gp = GraphedPipeline(model, geometry_streams=4 if gb == 1 else 2 if cfg == "stress" else 1,
+                             geometry_batches=gb, fuse=fuse, nslots=max(16, 4 * gb),
+                             geometry_bq=False if gb == 1 else None,
+                             tail_streams=2 if gb == 1 else None)
         outs = gp.run([xd] * n, [(md,)] * n if takes_mean else None)
     torch.cuda.synchronize()
     want = eager[0] if len(models) == 1 else tuple(eager)
@@ -296,7 +300,10 @@ def test_pose_rank_shards_pipeline_equals_unsharded(gb, fuse, monkeypatch):
         monkeypatch.setattr(shard, "draw_start", fixed_draw)
         monkeypatch.setattr(shard, "draw_start_into", lambda dst, N_: dst.copy_(fixed_draw(dst.shape[0], N_)))
         with torch.no_grad(), pn2.mlp_precision(prec), shard.batch_shard(B, lo):
-            gp = GraphedPipeline(model, geometry_batches=gb, fuse=fuse, nslots=max(8, 4 * gb))
+            gp = GraphedPipeline(model, geometry_batches=gb, fuse=fuse, nslots=max(16, 4 * gb),
+                                 geometry_streams=4 if gb == 1 else 1,
+                                 geometry_bq=False if gb == 1 else None,
+                             tail_streams=2 if gb == 1 else None)
             outs = gp.run([xd[lo:hi]] * n, [(md[lo:hi],)] * n)
         torch.cuda.synchronize()
         del gp

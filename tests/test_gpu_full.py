@@ -99,12 +99,15 @@ def test_full_size_head_eager_matches_reference(name):
     _check(g, acts, tags, out)
 
 
+@pytest.mark.parametrize("mode", ["fused4", "one"])
 @pytest.mark.parametrize("name", FULL)
-def test_full_size_head_graphed_pipeline_matches_reference(name, monkeypatch):
+def test_full_size_head_graphed_pipeline_matches_reference(name, mode, monkeypatch):
     """GraphedPipeline over four batches of the golden's input: the first runs eagerly and
     captures the slots, the rest replay the fps / sa / head graphs on their streams.  Every
     batch takes the golden's start draws (shard.draw_start patched to cycle them), so every
-    batch must reproduce the reference's outputs."""
+    batch must reproduce the reference's outputs.  mode: the class defaults (four batches fused
+    per launch), or bench.py's headline launch (one batch per launch, four geometry streams, the
+    ball queries in each batch's forward)."""
     from pn2 import shard
     from pn2.pipeline import GraphedPipeline
     g, model, args, draws, fseed = _setup(name)
@@ -121,7 +124,9 @@ def test_full_size_head_graphed_pipeline_matches_reference(name, monkeypatch):
     acts, tags, hs = _hook_acts(model)  # fire on the eager first batch only (graphs replay)
     n = 4
     extras = [tuple(args[1:])] * n if len(args) > 1 else None
-    gp = GraphedPipeline(model)
+    gp = GraphedPipeline(model) if mode == "fused4" else GraphedPipeline(
+        model, geometry_batches=1, fuse=False, nslots=16, geometry_streams=4, geometry_bq=False,
+        tail_streams=2)
     outs = gp.run([args[0]] * n, extras)
     torch.cuda.synchronize()
     for h in hs:
