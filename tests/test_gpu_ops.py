@@ -249,6 +249,25 @@ def test_index_points_out_of_range_is_nan_and_flagged():
         pn2.check_device_errors()
 
 
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs")
+def test_device_error_goes_to_the_launch_streams_device():
+    """a model on cuda:1 launched while cuda:0 is the current device raises its
+    device error bits into cuda:1's slot (the slot follows the launch stream's device,
+    hipStreamGetDevice), and cuda:0's check stays clean."""
+    import pn2
+    torch.cuda.set_device(0)
+    d1 = torch.device("cuda", 1)
+    pn2.check_device_errors("cuda:0")
+    pn2.check_device_errors(d1)
+    pts = torch.randn(2, 16, 3, device=d1)
+    got = pn2.index_points(pts, torch.tensor([[0, 16, 1], [-17, 2, 3]], device=d1))
+    assert torch.cuda.current_device() == 0
+    assert torch.isnan(got[0, 1]).all() and torch.isnan(got[1, 0]).all()
+    pn2.check_device_errors("cuda:0")
+    with pytest.raises(IndexError, match="out of range"):
+        pn2.check_device_errors(d1)
+
+
 @pytest.mark.parametrize("mid", [256, 512])
 @pytest.mark.parametrize("C,N", [(3, 1024), (3, 512), (3, 300), (10, 1024), (6, 777)])
 def test_fps_mid_shapes_exact(mid, C, N):
