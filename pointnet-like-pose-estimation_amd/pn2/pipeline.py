@@ -136,13 +136,12 @@ def _streams(device, geometry_cus):
         tail = torch.cuda.Stream(dev, priority=min(lo, hi) if tuning.get("tail_prio") else 0)
         main2 = torch.cuda.default_stream(dev)
         tail2 = torch.cuda.Stream(dev, priority=min(lo, hi) if tuning.get("tail_prio") else 0)
-        main3 = torch.cuda.Stream(dev)
         for st in (geo, main, tail):
             with torch.cuda.stream(st):
                 torch.zeros(1, device=dev)
             st.synchronize()
         _partitions[key] = (geo, main, tail, ())
-        _extra[device] = (geo2, main2, tail2, main3)
+        _extra[device] = (geo2, main2, tail2)
     if key not in _partitions:
         ncu = _cu_count(device)
         per = max(1, min(int(geometry_cus) // _XCDS, ncu // _XCDS - 1))  # CUs per XCD
@@ -177,12 +176,12 @@ def _extra_geometry_streams(device, n):
 
 
 def _extra_compute_streams(device, n):
-    """n (0-2) more compute streams for GraphedPipeline(compute_streams=1+n) (created with the
-    others by _streams): the process's default stream, then one more."""
+    """n (0 or 1) more compute streams for GraphedPipeline(compute_streams=1+n) (created with
+    the others by _streams): the process's default stream."""
     if n <= 0:
         return []
     _streams(device, 0)
-    return [_extra[device][1], _extra[device][3]][:n]
+    return [_extra[device][1]][:n]
 
 
 def partition(device, geometry_cus):
@@ -534,8 +533,8 @@ class GraphedPipeline(PipelinedForward):
             raise ValueError("pn2.pipeline: geometry_streams is 1 to 4")
         if compute_streams is None:
             compute_streams = 2 if geometry_cus <= 0 else 1
-        if compute_streams not in (1, 2, 3):
-            raise ValueError("pn2.pipeline: compute_streams is 1, 2 or 3")
+        if compute_streams not in (1, 2):
+            raise ValueError("pn2.pipeline: compute_streams is 1 or 2")
         if compute_streams > 1 and geometry_cus > 0:
             raise ValueError("pn2.pipeline: compute_streams > 1 needs shared CUs (geometry_cus=0)")
         self.compute_streams = int(compute_streams)
