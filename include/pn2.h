@@ -120,8 +120,9 @@ int64_t pn2_packed_stride(int64_t C);
  *   out_pts    [B,S,C] float32 contiguous, or NULL   index_points(points, fps_idx)
  *   out_packed [B,S,cp] float32, or NULL         packed centroids (contiguous-layout ssq)
  *   pts_packed [B,N,cp] float32, or NULL         packed input points (input-layout ssq)
- * C <= 16 (else PN2_EUNSUPPORTED: the channel-sum orders pinned against the reference are
- * those of C <= 16).  The cloud is register-resident up to N = 16384 for C == 3, 8192 for
+ * C <= 64 (else PN2_EUNSUPPORTED: the reference's channel-sum orders are pinned to C = 64);
+ * 16 < C <= 64 always runs the streamed kernel (256 threads per cloud; the same workspace rule
+ * with the LDS holding up to 40896 distances).  The cloud is register-resident up to N = 16384 for C == 3, 8192 for
  * C == 10, 4096 for other C (past that, up to N = 16384, the channels after xyz are re-read
  * from pts each iteration unless they are constant over the cloud: one-hot), with S <= 8192.
  * Any other N or S runs the streamed kernel: the points re-read every iteration, the running
@@ -144,7 +145,8 @@ int pn2_fps_host_ws_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64
                         float *out_pts, float *out_packed, float *pts_packed, void *workspace,
                         int64_t workspace_bytes, void *stream);
 
-/* Pack a [B,N,C] strided view into [B,N,cp] with its ssq (see above). */
+/* Pack a [B,N,C] strided view into [B,N,cp] with its ssq (see above).  C <= 64, as for the
+ * ball query and square_distance below (else PN2_EUNSUPPORTED). */
 int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,
                         int64_t sn, int64_t sc, float *packed, void *stream);
 
@@ -153,7 +155,8 @@ int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64
  * pts_packed [B,N,cp], ctr_packed [B,S,cp] from pn2_pack_points_f32 / pn2_fps_f32.
  * out_idx [B,S,K] int64.  Any 1 <= K <= N (rows that fit a 96 KB LDS buffer are built there and
  * written out whole; longer ones are written in place).  K > N is rejected with PN2_EINVAL
- * (the reference raises IndexError). */
+ * (the reference raises IndexError).  16 < C <= 64: a register-light kernel that walks the
+ * records in index order per centroid (same results; not tuned -- no BASELINE config has it). */
 int pn2_ball_query_f32(const float *pts_packed, const float *ctr_packed, int64_t B, int64_t N,
                        int64_t S, int64_t C, double radius, int64_t K, int64_t *out_idx,
                        void *stream);

@@ -16,11 +16,17 @@
  *   - torch.sum(x**2, -1) over the channel axis depends on the memory layout of x:
  *       channel-contiguous rows ("contig", stride_c == 1):
  *         C < 8  : ATen row_sum with 4 accumulators, tail into acc0, then acc0+acc1+acc2+acc3
- *         C >= 8 : 8 lane partials over C/8 chunks, scalar tail summed first, then
- *                  tail + v0 + v1 + ... + v7 (sequential)
+ *         C >= 8 : 8 lane partials over the C/8 8-channel vectors -- whole blocks of 4
+ *                  vectors into 4 vector accumulators, the leftover vectors into the first,
+ *                  ((a0+a1)+a2)+a3 per lane (a plain sequential lane sum below C = 40) --,
+ *                  scalar tail summed first, then tail + v0 + v1 + ... + v7 (sequential)
  *       point-contiguous rows ("strided", stride_n == 1, i.e. the permute(0,2,1) view of a
- *       [B,C,N] tensor): points n < 16*floor(N/16) are summed sequentially over c, the
- *       scalar tail n >= 16*floor(N/16) uses the row_sum order above.
+ *       [B,C,N] tensor): points n < 32*floor(N/32) (n < 4 when N = 4..7, none when N < 4 or
+ *       8 <= N < 32) are summed sequentially within chunks of 16 channels and the chunk sums
+ *       added in order (plain sequential for C <= 17); the other points use the row_sum order
+ *       above.  (Rounds 1-5 had 16*floor(N/16): no golden had C >= 5, a strided layout and
+ *       N mod 32 >= 16; round 6's n48/n600/n20/n6 goldens pin it.)
+ *       (C > 16: pinned to C = 64 by tools/probe/sum_orders_past_16.py, the r24/r40/r64 goldens)
  *   - matmul(src, dst^T) = fmaf chain in k order starting from s0*d0 (MKL sgemm), except when
  *     S*N*C < 400, where ATen's naive bmm kernel accumulates unfused: ((0 + s0*d0) + s1*d1) ...
  *   - square_distance = ((-2*mm) + ssq(src)) + ssq(dst), each rounded to float32.
@@ -52,12 +58,14 @@ static float seqsum(const float *a, int64_t C) {
 
 static float contigsum(const float *a, int64_t C) {
     if (C < 8) return rowsum4(a, C);
-    int64_t nv = C / 8, i, k;
+    int64_t nv = C / 8, nb = nv / 4, i, j, k;
     float v[8];
     for (k = 0; k < 8; ++k) {
-        float s = 0.f;
-        for (i = 0; i < nv; ++i) s = s + a[8 * i + k];
-        v[k] = s;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (i = 0; i < nb; ++i)
+            for (j = 0; j < 4; ++j) acc[j] = acc[j] + a[8 * (4 * i + j) + k];
+        for (i = 4 * nb; i < nv; ++i) acc[0] = acc[0] + a[8 * i + k];
+        v[k] = nb > 0 ? ((acc[0] + acc[1]) + acc[2]) + acc[3] : acc[0];
     }
     float r = seqsum(a + 8 * nv, C - 8 * nv);
     for (k = 0; k < 8; ++k) r = r + v[k];
@@ -65,8 +73,17 @@ static float contigsum(const float *a, int64_t C) {
 }
 
 /* Sum of the C squared channel values of point n under the reference's layout rule. */
+static float chunk16sum(const float *a, int64_t C) {
+    float r = seqsum(a, C < 16 ? C : 16);
+    for (int64_t c0 = 16; c0 < C; c0 += 16) r = r + seqsum(a + c0, C - c0 < 16 ? C - c0 : 16);
+    return r;
+}
+
+/* strided rows summed by ATen's vectorised body: whole blocks of 32 points (4 for N = 4..7) */
+static int64_t body_points(int64_t N) { return N >= 32 ? (N / 32) * 32 : (N >= 4 && N < 8) ? 4 : 0; }
+
 static float layout_sum(const float *sq, int64_t C, int64_t n, int64_t N, int strided) {
-    if (strided) return (n < (N / 16) * 16) ? seqsum(sq, C) : rowsum4(sq, C);
+    if (strided) return (n < body_points(N)) ? chunk16sum(sq, C) : rowsum4(sq, C);
     return contigsum(sq, C);
 }
 

@@ -282,9 +282,91 @@ __global__ __launch_bounds__(64 * P) void ball_query_kernel(
     }
 }
 
+// Point dimensions 16 < C <= kMaxCWide: lanes = 64 centroids of one cloud as above; every lane
+// walks the cloud's packed records in index order (wave-uniform addresses: broadcast loads that
+// stay in L1/L2) and writes its first K hits straight into its output row.  Same distance,
+// test, hit order, padding, counts and error flag as ball_query_kernel, without the LDS
+// staging and segment prefix -- at these widths the scan is a few MFLOP per cloud, and a
+// register tile of 64+ channels per record would not leave room for one.
+constexpr int kBqWideCP = ((kMaxCWide + 1 + 3) / 4) * 4;
+
+template <typename OT>
+__global__ __launch_bounds__(64) void ball_query_wide_kernel(const float *__restrict__ pts,
+                                                             const float *__restrict__ ctr, int N, int S,
+                                                             int C, int cp, int small, int nr,
+                                                             const BqOut<OT> O, unsigned *__restrict__ err) {
+    const int gpc = (S + 63) >> 6;
+    const int b = blockIdx.x / gpc;
+    const int g0 = (blockIdx.x - b * gpc) * 64;
+    const int s = g0 + (int)threadIdx.x;
+    const bool valid = s < S;
+    const int64_t q = (int64_t)b * S + (valid ? s : g0);
+    float c[kBqWideCP];
+#pragma unroll
+    for (int k = 0; k < kBqWideCP; ++k) c[k] = k < cp ? ctr[q * cp + k] : 0.f;
+    float ssq_c = 0.f;
+#pragma unroll
+    for (int k = 1; k < kBqWideCP; ++k)
+        if (k == C) ssq_c = c[k];  // static register indices (no scratch)
+    int total[kBqMaxR], first[kBqMaxR];
+#pragma unroll
+    for (int rr = 0; rr < kBqMaxR; ++rr) {
+        total[rr] = (valid && rr < nr) ? 0 : O.K[rr];
+        first[rr] = N;
+    }
+    const float *P = pts + (int64_t)b * N * cp;
+    for (int n = 0; n < N; ++n) {
+        if ((n & 31) == 0) {  // the wave stops once all its centroids have every K
+            bool more = false;
+#pragma unroll
+            for (int rr = 0; rr < kBqMaxR; ++rr) more = more || (rr < nr && total[rr] < O.K[rr]);
+            if (__builtin_amdgcn_ballot_w64(more) == 0) break;
+        }
+        const float *p = P + (int64_t)n * cp;
+        float mm = __fmul_rn(c[0], p[0]);
+#pragma unroll
+        for (int k = 1; k < kBqWideCP - 1; ++k)
+            if (k < C) mm = small ? __fadd_rn(mm, __fmul_rn(c[k], p[k])) : __builtin_fmaf(c[k], p[k], mm);
+        const float d = __fadd_rn(__builtin_fmaf(-2.0f, mm, ssq_c), p[C]);
+#pragma unroll
+        for (int rr = 0; rr < kBqMaxR; ++rr) {
+            if (rr < nr && !(d > O.r2[rr]) && total[rr] < O.K[rr]) {
+                if (total[rr] == 0) first[rr] = n;
+                O.out[rr][q * O.K[rr] + total[rr]] = (OT)n;
+                ++total[rr];
+            }
+        }
+    }
+    if (!valid) return;
+#pragma unroll
+    for (int rr = 0; rr < kBqMaxR; ++rr) {
+        if (rr >= nr) break;
+        const int K = O.K[rr], cj = total[rr];
+        // no point within the radius: padded with index N, the reference's out-of-range pad
+        // (see ball_query_kernel)
+        if (cj == 0) atomicOr(err, (unsigned)PN2_DEVERR_NO_NEIGHBOUR);
+        OT *o = O.out[rr] + q * K;
+        for (int k = cj; k < K; ++k) o[k] = (OT)first[rr];
+        if (O.cnt[rr]) O.cnt[rr][q] = cj;
+    }
+}
+
 }  // namespace pn2
 
 using namespace pn2;
+
+template <typename OT>
+static int launch_bq_wide(const float *pp, const float *cp_, int64_t B, int64_t N, int64_t S, int64_t C, int nr,
+                          const BqOut<OT> &O, hipStream_t st) {
+    const int64_t nblk = B * ((S + 63) / 64);
+    PN2_REQUIRE(nblk < (int64_t)1 << 31, "pn2_ball_query_f32: too many centroids");
+    unsigned *err = error_word(st);
+    PN2_REQUIRE(err, "pn2_ball_query_f32: no device error slot");
+    hipLaunchKernelGGL(ball_query_wide_kernel<OT>, dim3((unsigned)nblk), dim3(64), 0, st, pp, cp_, (int)N, (int)S,
+                       (int)C, (int)pn2_packed_stride(C), (int)(S * N * C < 400), nr, O, err);
+    PN2_LAUNCH_CHECK("ball_query_wide_kernel");
+    return PN2_OK;
+}
 
 template <int CP, int CC, typename OT, int NR>
 static int launch_bq(const float *pp, const float *cp_, int64_t B, int64_t N, int64_t S,
@@ -362,9 +444,11 @@ static int ball_query_impl(const float *pts_packed, const float *ctr_packed, int
                            int32_t *const *out_cnt, void *stream) {
     PN2_REQUIRE(pts_packed && ctr_packed && out_idx && radius && Ks, "pn2_ball_query_f32: null pointer");
     PN2_REQUIRE(nr >= 1 && nr <= kBqMaxR, "pn2_ball_query_multi: 1..%d radii (got %d)", kBqMaxR, nr);
-    PN2_REQUIRE(B >= 0 && N >= 1 && S >= 0 && C >= 1 && C <= kMaxC,
+    PN2_REQUIRE(B >= 0 && N >= 1 && S >= 0 && C >= 1,
                 "pn2_ball_query_f32: bad shape B=%lld N=%lld S=%lld C=%lld", (long long)B,
                 (long long)N, (long long)S, (long long)C);
+    if (C > kMaxCWide)
+        return set_error(PN2_EUNSUPPORTED, "pn2_ball_query_f32: unsupported C=%lld (max %d)", (long long)C, kMaxCWide);
     BqOut<OT> O;
     memset(&O, 0, sizeof(O));
     for (int r = 0; r < nr; ++r) {
@@ -382,6 +466,7 @@ static int ball_query_impl(const float *pts_packed, const float *ctr_packed, int
     if (B == 0 || S == 0) return PN2_OK;
     hipStream_t st = as_stream(stream);
     const int64_t cp = pn2_packed_stride(C);
+    if (C > kMaxC) return launch_bq_wide<OT>(pts_packed, ctr_packed, B, N, S, C, nr, O, st);
 #define PN2_BQ(CPV, CC)                                                                               \
     if (cp == CPV && (CC == 0 || (C == CC && S * N * C >= 400)))                                      \
         return nr == 1 ? launch_bq<CPV, CC, OT, 1>(pts_packed, ctr_packed, B, N, S, C, O, st)         \
@@ -444,7 +529,10 @@ extern "C" int pn2_square_distance_f32(const float *src_packed, const float *dst
                                        int64_t B, int64_t S, int64_t N, int64_t C, float *out,
                                        void *stream) {
     PN2_REQUIRE(src_packed && dst_packed && out, "pn2_square_distance_f32: null pointer");
-    PN2_REQUIRE(B >= 0 && S >= 0 && N >= 0 && C >= 1 && C <= kMaxC, "pn2_square_distance_f32: bad shape");
+    PN2_REQUIRE(B >= 0 && S >= 0 && N >= 0 && C >= 1, "pn2_square_distance_f32: bad shape");
+    if (C > kMaxCWide)
+        return set_error(PN2_EUNSUPPORTED, "pn2_square_distance_f32: unsupported C=%lld (max %d)", (long long)C,
+                         kMaxCWide);
     const int64_t tot = B * S * N;
     if (tot == 0) return PN2_OK;
     hipLaunchKernelGGL(square_distance_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,

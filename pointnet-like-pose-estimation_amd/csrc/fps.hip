@@ -44,7 +44,12 @@ __global__ __launch_bounds__(NT) void fps_kernel(const FpsArgs F) {
 // barrier, every thread reduces the NW slots.  The centroid's coordinates are re-read from
 // the input (one broadcast load).  Indices go straight to out_idx; the output pass reads them
 // back with sc1 loads (stores of other waves of this workgroup).
+// Point dimensions past the register-resident kMaxC (16 < C <= kMaxCWide) always take this
+// kernel, with 256 threads: a point's channels, squares and the centroid are register arrays
+// of kMaxCWide entries (predicated on C), too many for 1024-thread workgroups.
 constexpr int kFpsStreamT = 1024;
+template <int CM>
+constexpr int fps_stream_threads() { return CM > kMaxC ? 256 : kFpsStreamT; }
 
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
 #pragma unroll
@@ -56,11 +61,11 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 }
 
 template <int CM, bool FIXED, bool DL>
-__global__ __launch_bounds__(kFpsStreamT) void fps_stream_kernel(
+__global__ __launch_bounds__(fps_stream_threads<CM>()) void fps_stream_kernel(
     const float *__restrict__ pts, int N, int Crt, int64_t sb, int64_t sn, int64_t sc, int kind,
     const FpsStart start, int S, int64_t *__restrict__ out_idx, float *__restrict__ out_pts,
     float *__restrict__ out_packed, float *__restrict__ pts_packed, int cp, unsigned *__restrict__ dist_ws) {
-    constexpr int NT = kFpsStreamT, NW = NT / 64;
+    constexpr int NT = fps_stream_threads<CM>(), NW = NT / 64;
     __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
     const int C = FIXED ? CM : Crt;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -276,8 +281,8 @@ static int dispatch_fps(const float *pts, int64_t B, int64_t N, int64_t C, int64
 
 // the register-resident kernels' limits (dispatch_fps); past them the streamed kernel
 static bool fps_resident(int64_t N, int64_t S) { return N <= 16384 && S <= kFpsMaxS; }
-static size_t fps_stream_lds(int64_t N) { return (size_t)2 * (kFpsStreamT / 64) * 8 + (size_t)N * 4; }
-static bool fps_stream_dl(int64_t N) { return fps_stream_lds(N) <= (size_t)160 * 1024; }
+static size_t fps_stream_lds(int64_t N, int nt = kFpsStreamT) { return (size_t)2 * (nt / 64) * 8 + (size_t)N * 4; }
+static bool fps_stream_dl(int64_t N, int nt = kFpsStreamT) { return fps_stream_lds(N, nt) <= (size_t)160 * 1024; }
 
 template <int CM, bool FIXED>
 static int launch_fps_stream(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb, int64_t sn,
@@ -285,17 +290,18 @@ static int launch_fps_stream(const float *pts, int64_t B, int64_t N, int64_t C, 
                              float *out_packed, float *pts_packed, unsigned *ws, hipStream_t st) {
     const int kind = layout_kind(sn, sc);
     const int cp = (int)pn2_packed_stride(C);
-    if (fps_stream_dl(N)) {
+    constexpr int NT = fps_stream_threads<CM>();
+    if (fps_stream_dl(N, NT)) {
         static const hipError_t attr = hipFuncSetAttribute(
             reinterpret_cast<const void *>(&fps_stream_kernel<CM, FIXED, true>),
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         PN2_REQUIRE(attr == hipSuccess, "pn2_fps_f32: LDS attribute: %s", hipGetErrorString(attr));
-        hipLaunchKernelGGL((fps_stream_kernel<CM, FIXED, true>), dim3((unsigned)B), dim3(kFpsStreamT),
-                           fps_stream_lds(N), st, pts, (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx,
+        hipLaunchKernelGGL((fps_stream_kernel<CM, FIXED, true>), dim3((unsigned)B), dim3(NT),
+                           fps_stream_lds(N, NT), st, pts, (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx,
                            out_pts, out_packed, pts_packed, cp, nullptr);
     } else {
-        hipLaunchKernelGGL((fps_stream_kernel<CM, FIXED, false>), dim3((unsigned)B), dim3(kFpsStreamT),
-                           fps_stream_lds(0), st, pts, (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx,
+        hipLaunchKernelGGL((fps_stream_kernel<CM, FIXED, false>), dim3((unsigned)B), dim3(NT),
+                           fps_stream_lds(0, NT), st, pts, (int)N, (int)C, sb, sn, sc, kind, start, (int)S, out_idx,
                            out_pts, out_packed, pts_packed, cp, ws);
     }
     PN2_LAUNCH_CHECK("fps_stream_kernel");
@@ -304,6 +310,7 @@ static int launch_fps_stream(const float *pts, int64_t B, int64_t N, int64_t C, 
 
 extern "C" int64_t pn2_fps_workspace_bytes(int64_t B, int64_t N, int64_t C, int64_t S) {
     if (B < 0 || N < 1 || C < 1 || S < 1) return -1;
+    if (C > kMaxC) return fps_stream_dl(N, fps_stream_threads<kMaxCWide>()) ? 0 : B * N * 4;
     return (fps_resident(N, S) || fps_stream_dl(N)) ? 0 : B * N * 4;
 }
 
@@ -313,7 +320,8 @@ static int fps_check(const float *pts, const int64_t *start, int64_t *out_idx, i
     PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && S >= 1 && N < INT32_MAX && S < INT32_MAX,
                 "pn2_fps_f32: bad shape B=%lld N=%lld C=%lld S=%lld", (long long)B, (long long)N, (long long)C,
                 (long long)S);
-    if (C > kMaxC) return set_error(PN2_EUNSUPPORTED, "pn2_fps_f32: unsupported C=%lld (max %d)", (long long)C, kMaxC);
+    if (C > kMaxCWide)
+        return set_error(PN2_EUNSUPPORTED, "pn2_fps_f32: unsupported C=%lld (max %d)", (long long)C, kMaxCWide);
     const int64_t need = pn2_fps_workspace_bytes(B, N, C, S);
     PN2_REQUIRE(workspace_bytes >= need && (need == 0 || workspace),
                 "pn2_fps_f32: N=%lld needs pn2_fps_workspace_bytes = %lld bytes of workspace", (long long)N,
@@ -325,6 +333,7 @@ static int fps_run(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb
                    const FpsStart &start, int64_t S, int64_t *out_idx, float *out_pts, float *out_packed,
                    float *pts_packed, void *workspace, hipStream_t st) {
 #define A pts, B, N, C, sb, sn, sc, start, S, out_idx, out_pts, out_packed, pts_packed
+    if (C > kMaxC) return launch_fps_stream<kMaxCWide, false>(A, static_cast<unsigned *>(workspace), st);
     if (!fps_resident(N, S)) {
         unsigned *ws = static_cast<unsigned *>(workspace);
         if (C == 3) return launch_fps_stream<3, true>(A, ws, st);
@@ -429,7 +438,9 @@ bool pn2::fps_side_block_args(const pn2_fps_side &f, size_t lds_avail, FpsArgs &
 extern "C" int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64_t C, int64_t sb,
                                    int64_t sn, int64_t sc, float *packed, void *stream) {
     PN2_REQUIRE(pts && packed, "pn2_pack_points_f32: null pointer");
-    PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1 && C <= kMaxC, "pn2_pack_points_f32: bad shape");
+    PN2_REQUIRE(B >= 0 && N >= 1 && C >= 1, "pn2_pack_points_f32: bad shape");
+    if (C > kMaxCWide)
+        return set_error(PN2_EUNSUPPORTED, "pn2_pack_points_f32: unsupported C=%lld (max %d)", (long long)C, kMaxCWide);
     if (B == 0) return PN2_OK;
     const int kind = layout_kind(sn, sc);
     const int64_t tot = B * N;
@@ -438,8 +449,11 @@ extern "C" int pn2_pack_points_f32(const float *pts, int64_t B, int64_t N, int64
     if (C == 3)
         hipLaunchKernelGGL(pack_points_kernel<3>, grid, dim3(256), 0, as_stream(stream), pts, B,
                            (int)N, 3, sb, sn, sc, kind, packed, cp);
-    else
+    else if (C <= kMaxC)
         hipLaunchKernelGGL(pack_points_kernel<kMaxC>, grid, dim3(256), 0, as_stream(stream), pts,
+                           B, (int)N, (int)C, sb, sn, sc, kind, packed, cp);
+    else
+        hipLaunchKernelGGL(pack_points_kernel<kMaxCWide>, grid, dim3(256), 0, as_stream(stream), pts,
                            B, (int)N, (int)C, sb, sn, sc, kind, packed, cp);
     PN2_LAUNCH_CHECK("pack_points_kernel");
     return PN2_OK;

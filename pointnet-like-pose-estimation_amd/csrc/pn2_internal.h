@@ -88,7 +88,8 @@ bool is_default_error_slot(const unsigned *slot);
 // lost) into slot[1], copied to *bits; stream-ordered on st, which it then waits for
 hipError_t take_errors(unsigned *slot, int clear, unsigned *bits, hipStream_t st);
 
-constexpr int kMaxC = 16;  // point dims (xyz + one-hot) held in registers
+constexpr int kMaxC = 16;      // point dims (xyz + one-hot) of the register-resident kernels
+constexpr int kMaxCWide = 64;  // point dims of the streamed FPS / wide ball query (16 < C <= 64)
 
 // np: bf16 planes per operand -- 3 = fp32-accurate split products, 1 = plain bf16 products
 // sa_chain.hip: 1 launched, 0 not eligible, <0 error
@@ -118,9 +119,15 @@ int64_t chain_prepass_bytes(const pn2_sa_src &s, const pn2_mlp_layer *layers, in
 // --------------------------------------------------------------- device: reference sum orders
 // torch.sum(x**2, -1) over the channel axis, reproduced bit-for-bit (torch 2.10 CPU, AVX512);
 // pinned in oracle/pn2_oracle.c and tests/test_oracle_golden.py.
-//  contig  (stride_c == 1):  C<8 -> row_sum with 4 accumulators; C>=8 -> 8 lane partials,
-//                            scalar tail first, then tail+v0+...+v7.
-//  strided (stride_n == 1):  n < 16*floor(N/16) -> sequential; tail -> row_sum order.
+//  contig  (stride_c == 1):  C<8 -> row_sum with 4 accumulators; C>=8 -> 8 lane partials
+//                            (8-channel vectors: whole 32-channel blocks into 4 vector
+//                            accumulators, the leftover vectors into the first, then
+//                            ((a0+a1)+a2)+a3 per lane), scalar tail first, then tail+v0+...+v7.
+//  strided (stride_n == 1):  n < strided_body_points(N) (32*floor(N/32); 4 for N = 4..7) ->
+//                            sequential within 16-channel chunks, the chunk sums added in
+//                            order; the other points -> row_sum order.
+// (C > 16 pinned to C = 64 by tools/probe/sum_orders_past_16.py and the r24/r40/r64 goldens;
+// for C <= 16 both reduce to the plain forms.)
 // `a` is a register array; C is runtime (<= CM).
 // Element-wise adds in round-to-nearest.  The vector overload (two points per packed
 // v_pk_add_f32) is a plain add under `fp contract(off)` (no product may be fused into it).
@@ -168,9 +175,29 @@ __device__ __forceinline__ T contig_sum(const T (&a)[CM], int C) {
     T v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = T(0.f);
+    if constexpr (CM < 40) {
 #pragma unroll
-    for (int k = 0; k < CM; ++k)
-        if (k < nv8) v[k & 7] = add_rn(v[k & 7], a[k]);
+        for (int k = 0; k < CM; ++k)
+            if (k < nv8) v[k & 7] = add_rn(v[k & 7], a[k]);
+    } else {
+        // 4 vector accumulators over whole 32-channel blocks, leftover vectors into the first
+        const int nb32 = (C / 32) * 32;
+        T u[3][8];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) u[j][l] = T(0.f);
+#pragma unroll
+        for (int k = 0; k < CM; ++k) {
+            const int j = (k / 8) & 3;
+            if (k < nb32 && j > 0) u[j - 1][k & 7] = add_rn(u[j - 1][k & 7], a[k]);
+            else if (k < nv8) v[k & 7] = add_rn(v[k & 7], a[k]);
+        }
+        if (nb32 > 0) {
+#pragma unroll
+            for (int l = 0; l < 8; ++l) v[l] = add_rn(add_rn(add_rn(v[l], u[0][l]), u[1][l]), u[2][l]);
+        }
+    }
     T r = T(0.f);
 #pragma unroll
     for (int k = 0; k < CM; ++k)
@@ -180,12 +207,32 @@ __device__ __forceinline__ T contig_sum(const T (&a)[CM], int C) {
     return r;
 }
 
+// strided rows' body points: sequential within 16-channel chunks, chunk sums in order
+template <int CM, typename T>
+__device__ __forceinline__ T chunk16_sum(const T (&a)[CM], int C) {
+    if constexpr (CM <= 16) {
+        return seq_sum<CM>(a, C);
+    } else {
+        T r = T(0.f), s = T(0.f);
+#pragma unroll
+        for (int k = 0; k < CM; ++k) {
+            if (k < C) s = add_rn(s, a[k]);
+            if (k % 16 == 15 || k == CM - 1) {
+                if (k < 16) r = s;
+                else if (k - k % 16 < C) r = add_rn(r, s);
+                s = T(0.f);
+            }
+        }
+        return r;
+    }
+}
+
 // sum of squares of one row in the order ATen uses for its layout/position (rule: 0 contiguous,
-// 1 strided sequential, 2 strided tail)
+// 1 strided body, 2 strided tail)
 template <int CM, typename T>
 __device__ __forceinline__ T layout_sum(const T (&a)[CM], int C, int rule) {
     if (rule == 0) return contig_sum<CM>(a, C);
-    if (rule == 1) return seq_sum<CM>(a, C);
+    if (rule == 1) return chunk16_sum<CM>(a, C);
     return rowsum4<CM>(a, C);
 }
 
@@ -198,9 +245,15 @@ __host__ __device__ __forceinline__ int layout_kind(int64_t sn, int64_t sc) {
     return (sc != 1 && sn == 1) ? 1 : 0;  // 1: point-contiguous ("strided") rows
 }
 
+// the strided rows summed by ATen's vectorised body: whole blocks of 32 points, or the first 4
+// of a 4..7-point cloud (measured round 6 over N = 2..2064, C = 5..64; C <= 4 every order agrees)
+__host__ __device__ __forceinline__ int64_t strided_body_points(int64_t N) {
+    return N >= 32 ? (N / 32) * 32 : (N >= 4 && N < 8) ? 4 : 0;
+}
+
 __device__ __forceinline__ int point_rule(int kind, int64_t n, int64_t N) {
     if (kind == 0) return 0;
-    return (n < (N / 16) * 16) ? 1 : 2;
+    return (n < strided_body_points(N)) ? 1 : 2;
 }
 
 // ----------------------------------------------------------------- device: wave reductions

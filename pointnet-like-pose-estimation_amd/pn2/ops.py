@@ -482,7 +482,8 @@ def sa_mlp_max_impl(out, mode, points, feature, centers, idx, wts, alphas, betas
         raise ValueError("pn2::sa_mlp_max_: precision must be one of %s" % (PRECISIONS,))
     bf16 = precision == "bf16"
     if bf16 and not splits:
-        raise ValueError("pn2::sa_mlp_max_: bf16 needs the split weight images")
+        raise ValueError("pn2::sa_mlp_max_: bf16 needs the split weight images (none for points "
+                         "with more than 16 channels)")
     if mode == _lib.SRC_ROWS:
         _dev(rows, "pn2::sa_mlp_max_")
         if rows.dim() != 3 or rows.stride(2) != 1 or rows.stride(0) != rows.shape[1] * rows.stride(1):

@@ -129,12 +129,18 @@ def _needs_autograd(module, *tensors):
     return any(p.requires_grad for p in module.parameters())
 
 
+_SPLIT_MAX_XYZ = 16  # point channels of a split-bf16 first layer (csrc/sa_chain.hip)
+
+
 def _pack_chain(convs, bns, cache, rot0, xyz=0, xyz_first=True):
     """Fold each Conv2d-1x1 + eval BatchNorm2d into (W^T, alpha, beta) for the fp32 kernels and
     the split-bf16 image for the chain kernel; cached until any parameter/buffer changes
     (data_ptr or in-place version).  rot0: xyz channels leading the first layer's input in the
     reference's order (the fp32 kernels put them behind the features); xyz / xyz_first: the
-    first layer's xyz channel count and order for the chain kernel (rows [xyz | features])."""
+    first layer's xyz channel count and order for the chain kernel (rows [xyz | features]).
+    Points with more than 16 channels get no split images: the split-bf16 kernels hold at most
+    16 point channels (pn2_layer_split_kblocks), so those layers run the fp32 kernels only and
+    precision "bf16" fails loudly for them (sa_mlp_max_impl)."""
     tensors = []
     for conv, bn in zip(convs, bns):
         tensors += [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
@@ -151,8 +157,9 @@ def _pack_chain(convs, bns, cache, rot0, xyz=0, xyz_first=True):
                 als.append(al)
                 bes.append(be)
                 cins.append(conv.weight.shape[1])
-                splits.append(ops.pack_layer_split_direct(conv.weight, xyz if li == 0 else 0,
-                                                   xyz_first))
+                if xyz <= _SPLIT_MAX_XYZ:
+                    splits.append(ops.pack_layer_split_direct(conv.weight, xyz if li == 0 else 0,
+                                                              xyz_first))
         cache["key"] = key
         cache["layers"] = (wts, als, bes, cins, splits)
     return cache["layers"]

@@ -17,11 +17,12 @@ def cloud(kind, B, N, seed, labels=None):
       'dup3'      uniform, then provider.random_point_dropout-style duplication of point 0
                   (/root/reference/provider.py:157-164): many exact duplicates -> FPS ties
       'onehot10'  xyz + 7-way one-hot of `labels` (provider.splice_torch, provider.py:166-180)
-      'randn10'   N(0,1) in all 10 channels (not a real input; pins the channel-sum order)
+      'randn<C>'  N(0,1) in all C channels (not a real input; pins the channel-sum order:
+                  randn10, and randn24 / randn40 / randn64 past the register-resident C <= 16)
     """
     g = torch.Generator().manual_seed(seed)
-    if kind == 'randn10':
-        return torch.randn(B, N, 10, generator=g)
+    if kind.startswith('randn'):
+        return torch.randn(B, N, int(kind[5:]), generator=g)
     xyz = torch.rand(B, N, 3, generator=g) * 2 - 1
     if kind == 'dup3':
         for b in range(B):
@@ -94,6 +95,20 @@ INDEX_CASES = {
     # the reference's real scans (points stored in the fixture): clustered, non-uniform density
     'camera_strided': ('camera', 2, 10000, 'strided', 512, [(0.2, 32), (0.1, 16), (0.4, 128)], 22),
     'camera10_contig': ('camera10', 2, 10000, 'contig', 512, [(0.2, 32), (0.4, 64)], 23),
+    # point dimensions past the register-resident 16 (the streamed FPS, the wide ball query):
+    # both layouts, N off the 16-point strided-tail boundary, radii around the median distance
+    'r24_contig':   ('randn24', 2, 1000, 'contig', 256, [(6.0, 32), (7.5, 64)], 24),
+    'r24_strided':  ('randn24', 2, 1000, 'strided', 256, [(6.0, 32), (7.5, 64)], 25),
+    'r40_contig':   ('randn40', 2, 600, 'contig', 128, [(8.0, 32), (9.5, 64)], 26),
+    'r40_strided':  ('randn40', 1, 600, 'strided', 128, [(8.0, 32), (9.5, 64)], 27),
+    'r64_contig':   ('randn64', 1, 500, 'contig', 128, [(10.5, 32), (12.0, 64)], 28),
+    'r64_strided':  ('randn64', 2, 500, 'strided', 128, [(10.5, 32), (12.0, 64)], 29),
+    # strided clouds whose point count is not a multiple of 32: ATen sums whole 32-point
+    # blocks vectorised (the first 4 points of a 4..7-point cloud), the rest in row_sum order
+    'r10_n600_strided': ('randn10', 1, 600, 'strided', 128, [(2.0, 32), (3.0, 64)], 30),
+    'r10_n48_strided':  ('randn10', 3, 48, 'strided', 16, [(3.0, 8), (4.0, 16)], 31),
+    'r10_n20_strided':  ('randn10', 3, 20, 'strided', 8, [(3.0, 4), (4.5, 20)], 32),
+    'r10_n6_strided':   ('randn10', 4, 6, 'strided', 6, [(3.0, 2), (5.0, 6)], 33),
 }
 
 # head-level cases: name -> (head, B, N, cloud kind, weight seed, forward seed)
@@ -210,6 +225,25 @@ TRAIN_CASES = {
     'group_all': ('ssg', (None, None, None, 3 + 32, [64, 128], True), 3, 128, 32, 502, 602),
     'msg': ('msg', (32, [8, 16], [0.3, 0.6], 16, [[16, 32], [32, 32]]), 2, 256, 16, 503, 603),
 }
+
+
+# eval-mode SA layers on points with more than 16 channels (the streamed FPS, the wide ball
+# query, the generic MLP path): name -> (kind, ctor args, B, N, C, D, weight seed, forward seed).
+# points [B, C, N] and features [B, D, N] are N(0,1) (sa_inputs); radii around the median
+# distance of C-dimensional normal points.  MSG in_channel = D, num_category = C - 3.
+SA_WIDE_CASES = {
+    'ssg_c24': ('ssg', (64, 32, 6.0, 24 + 8, [32, 64], False), 2, 512, 24, 8, 700, 800),
+    'ssg_c40_xyz': ('ssg', (32, 16, 8.5, 40, [32, 32, 64], False), 2, 300, 40, 0, 701, 801),
+    'group_all_c20': ('ssg', (None, None, None, 20 + 16, [64, 128], True), 3, 128, 20, 16, 702, 802),
+    'msg_c24': ('msg', (32, [8, 16], [5.5, 7.0], 8, [[32, 32], [32, 64]], 21), 2, 256, 24, 8, 703, 803),
+}
+
+
+def sa_inputs(B, N, C, D, seed):
+    """points [B, C, N] and feature [B, D, N] (or None), N(0,1), channel-first."""
+    g = torch.Generator().manual_seed(seed)
+    pts = torch.randn(B, C, N, generator=g)
+    return pts, (torch.randn(B, D, N, generator=g) if D else None)
 
 
 # PointNet-v1 training cases: name -> (head module, B, N, cloud kind, weight seed, get_model

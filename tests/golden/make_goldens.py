@@ -20,6 +20,7 @@ Files:
                     (cases.E2E_CASE), the reference's whole test-script input path
   prep_<case>.npz   input preparation (cases.PREP_CASES) by provider.py's own functions
   train_<case>.npz  training-mode SA forward + backward (cases.TRAIN_CASES)
+  sa_<case>.npz     eval-mode SA layers on points with C > 16 channels (cases.SA_WIDE_CASES)
 (`make_goldens.py v1` regenerates only the v1 files, etc.)
   meta.json         torch version, CPU capability, MKL/oneDNN versions, thread count
 """
@@ -324,6 +325,30 @@ def gen_train(P):
         print("train", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
 
 
+def gen_sa(P):
+    """Eval-mode SA layers on points with more than 16 channels (cases.SA_WIDE_CASES): the
+    reference module's centroids and features."""
+    for name, (kind, args, B, N, C, D, wseed, fseed) in cases.SA_WIDE_CASES.items():
+        if only_cases and name not in only_cases:
+            continue
+        ctor = P.PointNetSetAbstraction if kind == 'ssg' else P.PointNetSetAbstractionMsg
+        torch.manual_seed(wseed)
+        mod = ctor(*args)
+        cases.randomize_bn(mod, wseed + 1)
+        mod.eval()
+        pts, feat = cases.sa_inputs(B, N, C, D, wseed + 2)
+        rec = {"points": pts.numpy(), "state_hash": np.array(cases.state_hash(mod))}
+        if feat is not None:
+            rec["feature"] = feat.numpy()
+        torch.manual_seed(fseed)
+        with torch.no_grad():
+            new_points, new_feature = mod(pts, feat)
+        rec["new_points"] = new_points.numpy()
+        rec["new_feature"] = new_feature.numpy()
+        np.savez_compressed(os.path.join(HERE, "sa_%s.npz" % name), **rec)
+        print("sa", name, {k: v.shape for k, v in rec.items() if hasattr(v, "shape")})
+
+
 def _v1_step_record(model, x, Rs, prefix, rec):
     """One train step of a v1 head (loss = sum_i out_i * R_i; R drawn here when Rs is empty):
     outputs, parameter gradients (large ones as a fixed sample + norm) under `prefix`."""
@@ -403,7 +428,7 @@ only_cases = set()  # `make_goldens.py full cls_ssg_b32`: just these cases of th
 def main():
     torch.set_num_threads(8)
     P, importlib = _ref()
-    kinds = ("index", "heads", "full", "e2e", "v1", "prep", "train", "trainv1")
+    kinds = ("index", "heads", "full", "e2e", "v1", "prep", "train", "trainv1", "sa")
     only = [a for a in sys.argv[1:] if a in kinds]
     only_cases.update(a for a in sys.argv[1:] if a not in kinds)
     if not only or "index" in only:
@@ -422,6 +447,8 @@ def main():
         gen_train(P)
     if not only or "trainv1" in only:
         gen_train_v1(importlib)
+    if not only or "sa" in only:
+        gen_sa(P)
     meta = {
         "torch": torch.__version__,
         "cpu_capability": torch.backends.cpu.get_cpu_capability(),

@@ -42,7 +42,7 @@ def test_validation_errors_without_gpu():
     assert rc == -1 and b"null" in L.pn2_last_error()
     rc = L.pn2_ball_query_f32(1, 1, 2, 8, 4, 3, 0.2, 9, 1, None)
     assert rc == -1 and b"sample_number 9 > N 8" in L.pn2_last_error()
-    rc = L.pn2_fps_f32(1, 1, 8, 40, 320, 40, 1, 1, 4, 1, None, None, None, None)
+    rc = L.pn2_fps_f32(1, 1, 8, 65, 520, 65, 1, 1, 4, 1, None, None, None, None)
     assert rc == -2 and b"unsupported C" in L.pn2_last_error()
 
 

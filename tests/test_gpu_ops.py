@@ -84,7 +84,7 @@ def test_square_distance_bit_exact(name):
 
 @pytest.mark.parametrize("C,layout", [(3, "strided"), (3, "contig"), (6, "contig"), (10, "strided"),
                                       (13, "contig"), (16, "strided")])
-@pytest.mark.parametrize("N", [1, 2, 63, 65, 300, 1000, 2049, 4096])
+@pytest.mark.parametrize("N", [1, 2, 6, 20, 48, 63, 65, 300, 600, 1000, 2049, 4096])
 def test_fps_and_ball_query_random_vs_oracle(C, layout, N):
     import pn2
     gen = torch.Generator().manual_seed(1000 * C + N)
@@ -154,7 +154,7 @@ def test_errors_are_loud():
     with pytest.raises(RuntimeError):
         pn2.farthest_point_sample(torch.rand(1, 8, 3), 4)  # CPU tensor: no CPU path
     with pytest.raises(Pn2Error):
-        torch.ops.pn2.fps(torch.rand(1, 8, 40, device=DEV), 4, torch.zeros(1, dtype=torch.long, device=DEV))
+        torch.ops.pn2.fps(torch.rand(1, 8, 65, device=DEV), 4, torch.zeros(1, dtype=torch.long, device=DEV))
 
 
 def test_fps_stress_size_vs_oracle():
