@@ -136,12 +136,17 @@ def _streams(device, geometry_cus):
         tail = torch.cuda.Stream(dev, priority=min(lo, hi) if tuning.get("tail_prio") else 0)
         main2 = torch.cuda.default_stream(dev)
         tail2 = torch.cuda.Stream(dev, priority=min(lo, hi) if tuning.get("tail_prio") else 0)
+        # one more normal-priority stream, never used: creating it moves the hardware queues
+        # the later geometry streams (_extra_geometry_streams) get, and without it the headline
+        # pipeline loses 15-25 % (r06, same box, interleaved: K = 20 117-122k with it, 88-99k
+        # without; tools/ab_worktree.sh)
+        spare = torch.cuda.Stream(dev)
         for st in (geo, main, tail):
             with torch.cuda.stream(st):
                 torch.zeros(1, device=dev)
             st.synchronize()
         _partitions[key] = (geo, main, tail, ())
-        _extra[device] = (geo2, main2, tail2)
+        _extra[device] = (geo2, main2, tail2, spare)
     if key not in _partitions:
         ncu = _cu_count(device)
         per = max(1, min(int(geometry_cus) // _XCDS, ncu // _XCDS - 1))  # CUs per XCD
